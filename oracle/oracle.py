@@ -1,0 +1,100 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of the CPU restatement (oracle/src/oracle.cpp) of the
+reference's per-pixel trace loop. Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg may import this module, and only as the checker.
+
+Parity status (see DESIGN.md "Oracle"): the Java reference cannot be built or
+run in this container (no JDK), so the restatement is pinned by the
+hand-derived known-answer pixels of SURVEY.md 8(c) and by golden fixtures it
+generates (tests/golden/, script tests/golden/make_golden.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB_PATH = ORACLE_DIR / "build" / "liboracle.so"
+
+ST_NAMES = ["camera", "shadow", "refl", "refr", "box", "tri", "quad", "sphere", "light", "photon", "texel"]
+
+_lib = None
+
+
+def build(force: bool = False) -> Path:
+    """Compile the oracle with its Makefile (gcc, -ffp-contract=off)."""
+    if force or not LIB_PATH.exists():
+        subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(str(LIB_PATH))
+        L.oracle_last_error.restype = ctypes.c_char_p
+        L.oracle_register_texture.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.oracle_load.restype = ctypes.c_void_p
+        L.oracle_load.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.oracle_free.argtypes = [ctypes.c_void_p]
+        L.oracle_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_build_photons.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.oracle_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+class OracleScene:
+    """A .cli scene loaded by the oracle's own loader (myRTFileReader restatement)."""
+
+    def __init__(self, scene_dir: str | os.PathLike, cli: str, textures: dict | None = None):
+        L = lib()
+        for name, arr in (textures or {}).items():
+            a = np.ascontiguousarray(arr, dtype=np.uint8)
+            L.oracle_register_texture(name.encode(), a.shape[1], a.shape[0], a.ctypes.data)
+        self._h = L.oracle_load(str(scene_dir).encode(), cli.encode())
+        if not self._h:
+            raise RuntimeError("oracle load failed: " + L.oracle_last_error().decode())
+
+    def info(self) -> dict:
+        v = np.zeros(8, dtype=np.int64)
+        lib().oracle_info(self._h, v.ctypes.data, 8)
+        keys = ["objects", "lights", "bvh_internal", "bvh_leaves", "bvh_depth", "bvh_prims", "prims", "rays_per_pixel"]
+        return dict(zip(keys, v.tolist()))
+
+    def build_photons(self, seed: int) -> int:
+        return lib().oracle_build_photons(self._h, seed)
+
+    def render(self, W: int, H: int, spp: int = 0, seed: int = 0x5EED0001, rows=None, row_step: int = 1,
+               threads: int = 0):
+        """Returns (rgb float32 [n,W,3], argb int32 [n,W], stats dict) for rows[0]:rows[1]:row_step."""
+        r0, r1 = (0, H) if rows is None else rows
+        n = len(range(r0, r1, row_step))
+        rgb = np.zeros((n, W, 3), dtype=np.float32)
+        argb = np.zeros((n, W), dtype=np.int32)
+        st = np.zeros(16, dtype=np.uint64)
+        nt = threads if threads > 0 else (os.cpu_count() or 1)
+        rc = lib().oracle_render(self._h, W, H, spp, seed, r0, r1, row_step, rgb.ctypes.data, argb.ctypes.data,
+                                 st.ctypes.data, nt)
+        if rc != 0:
+            raise RuntimeError("oracle render failed")
+        return rgb, argb, dict(zip(ST_NAMES, st[: len(ST_NAMES)].tolist()))
+
+    def close(self):
+        if self._h:
+            lib().oracle_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,255 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY -- never linked into the product library.
+//
+// Java-semantics scalar, vector and matrix helpers for the CPU restatement of
+// jturner65/distRayTracer_old (reference mounted read-only at /root/reference).
+// Every expression keeps the reference's evaluation order so that, built with
+// -O2 -ffp-contract=off (no FMA contraction, no fast-math), results follow the
+// Java double arithmetic of the reference.
+//
+//   myVector            src/rayTracerDistAccelShdPhtnMap/myVector.java:7-63
+//   myMatrix            src/rayTracerDistAccelShdPhtnMap/myVector.java:65-223
+//   myMatStack          src/rayTracerDistAccelShdPhtnMap/myVector.java:225-256
+//   p.min / p.max       src/rayTracerDistAccelShdPhtnMap/DistRayTracer.java:424-425
+//   rotVecAroundAxis    src/rayTracerDistAccelShdPhtnMap/DistRayTracer.java:336-349
+//   getOrthoVec         src/rayTracerDistAccelShdPhtnMap/DistRayTracer.java:455-462
+#pragma once
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+
+namespace orc {
+
+static const double EPS = 0.0000001;                       // DistRayTracer.java:53
+// Processing PConstants are floats widened into double math.
+static const double PI_F = (double)3.14159265358979323846f;
+static const double TWO_PI_F = (double)6.28318530717958647692f;
+static const double DEG_TO_RAD_F = (double)(3.14159265358979323846f / 180.0f);
+static const double DMAX = std::numeric_limits<double>::max();
+
+// java.lang.Math.min/max (NaN-propagating, -0.0 < 0.0)
+static inline double jmin(double a, double b) {
+  if (a != a) return a;
+  if (a == 0.0 && b == 0.0) return std::signbit(a) ? a : b;
+  return (a <= b) ? a : b;
+}
+static inline double jmax(double a, double b) {
+  if (a != a) return a;
+  if (a == 0.0 && b == 0.0) return std::signbit(a) ? b : a;
+  return (a >= b) ? a : b;
+}
+// (int) cast of a double in Java: NaN -> 0, saturating.
+static inline int32_t jd2i(double v) {
+  if (v != v) return 0;
+  if (v >= 2147483647.0) return 2147483647;
+  if (v <= -2147483648.0) return (int32_t)0x80000000;
+  return (int32_t)v;
+}
+// Double.compare total order (-0.0 < 0.0, NaN greatest); used by TreeMap<Double>
+static inline int jdcompare(double a, double b) {
+  if (a < b) return -1;
+  if (a > b) return 1;
+  int64_t ab, bb;
+  std::memcpy(&ab, &a, 8);
+  std::memcpy(&bb, &b, 8);
+  if (a != a) ab = 0x7ff8000000000000LL;
+  if (b != b) bb = 0x7ff8000000000000LL;
+  return ab == bb ? 0 : (ab < bb ? -1 : 1);
+}
+
+struct V3 {
+  double x = 0, y = 0, z = 0;
+  V3() {}
+  V3(double a, double b, double c) : x(a), y(b), z(c) {}
+};
+static inline V3 vsub(const V3& p, const V3& q) { return V3(p.x - q.x, p.y - q.y, p.z - q.z); }
+static inline V3 vadd(const V3& p, const V3& q) { return V3(p.x + q.x, p.y + q.y, p.z + q.z); }
+static inline V3 vmul(const V3& p, double n) { return V3(p.x * n, p.y * n, p.z * n); }
+static inline double dot(const V3& a, const V3& b) { return ((a.x * b.x) + (a.y * b.y)) + (a.z * b.z); }
+static inline V3 cross(const V3& a, const V3& b) {
+  return V3((a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x));
+}
+static inline double sqmag(const V3& a) { return ((a.x * a.x) + (a.y * a.y)) + (a.z * a.z); }
+static inline double mag(const V3& a) { return std::sqrt(sqmag(a)); }
+// myVector._normalize: no-op on zero, divides (not reciprocal multiply)
+static inline void normalize_ip(V3& a) {
+  double m = mag(a);
+  if (m == 0) return;
+  a.x /= m; a.y /= m; a.z /= m;
+}
+static inline V3 normalized(const V3& a) {
+  double m = mag(a);
+  if (m == 0) return V3(0, 0, 0);
+  return V3(a.x / m, a.y / m, a.z / m);
+}
+static inline double dist(const V3& p, const V3& q) {
+  return std::sqrt((((p.x - q.x) * (p.x - q.x)) + ((p.y - q.y) * (p.y - q.y))) + ((p.z - q.z) * (p.z - q.z)));
+}
+static inline double comp(const V3& v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+
+struct M4 {
+  double m[4][4];
+  M4() { ident(); }
+  void ident() { for (int r = 0; r < 4; ++r) for (int c = 0; c < 4; ++c) m[r][c] = (r == c) ? 1.0 : 0.0; }
+  void zero() { for (int r = 0; r < 4; ++r) for (int c = 0; c < 4; ++c) m[r][c] = 0.0; }
+};
+// this x b, accumulating from 0 exactly as myMatrix.multMat
+static inline M4 mmul(const M4& a, const M4& b) {
+  M4 r;
+  for (int row = 0; row < 4; ++row)
+    for (int col = 0; col < 4; ++col) {
+      double acc = 0;
+      for (int k = 0; k < 4; ++k) acc += a.m[row][k] * b.m[k][col];
+      r.m[row][col] = acc;
+    }
+  return r;
+}
+static inline void mvert(const M4& a, const double b[4], double out[4]) {
+  for (int row = 0; row < 4; ++row) {
+    double acc = 0;
+    for (int col = 0; col < 4; ++col) acc += a.m[row][col] * b[col];
+    out[row] = acc;
+  }
+}
+static inline V3 xpt(const M4& a, const V3& p) {
+  double b[4] = {p.x, p.y, p.z, 1}, o[4];
+  mvert(a, b, o);
+  return V3(o[0], o[1], o[2]);
+}
+static inline V3 xvec(const M4& a, const V3& p) {
+  double b[4] = {p.x, p.y, p.z, 0}, o[4];
+  mvert(a, b, o);
+  return V3(o[0], o[1], o[2]);
+}
+static inline M4 transpose(const M4& a) {
+  M4 r;
+  for (int row = 0; row < 4; ++row) for (int col = 0; col < 4; ++col) r.m[col][row] = a.m[row][col];
+  return r;
+}
+// Cofactor ("pairs") inverse of myMatrix.InvertMe (myVector.java:111-196).
+// For |det| <= 1e-7 the reference returns its fresh `new myMatrix()`, i.e. the
+// IDENTITY (myVector.java:68-72,116,192-195).
+static inline M4 invert(const M4& a) {
+  double tmp[12], src[16], dst[16];
+  for (int row = 0; row < 4; ++row) for (int col = 0; col < 4; ++col) src[4 * col + row] = a.m[row][col];
+  tmp[0] = src[10] * src[15]; tmp[1] = src[11] * src[14]; tmp[2] = src[9] * src[15];
+  tmp[3] = src[11] * src[13]; tmp[4] = src[9] * src[14]; tmp[5] = src[10] * src[13];
+  tmp[6] = src[8] * src[15]; tmp[7] = src[11] * src[12]; tmp[8] = src[8] * src[14];
+  tmp[9] = src[10] * src[12]; tmp[10] = src[8] * src[13]; tmp[11] = src[9] * src[12];
+  dst[0] = tmp[0] * src[5] + tmp[3] * src[6] + tmp[4] * src[7];
+  dst[0] -= tmp[1] * src[5] + tmp[2] * src[6] + tmp[5] * src[7];
+  dst[1] = tmp[1] * src[4] + tmp[6] * src[6] + tmp[9] * src[7];
+  dst[1] -= tmp[0] * src[4] + tmp[7] * src[6] + tmp[8] * src[7];
+  dst[2] = tmp[2] * src[4] + tmp[7] * src[5] + tmp[10] * src[7];
+  dst[2] -= tmp[3] * src[4] + tmp[6] * src[5] + tmp[11] * src[7];
+  dst[3] = tmp[5] * src[4] + tmp[8] * src[5] + tmp[11] * src[6];
+  dst[3] -= tmp[4] * src[4] + tmp[9] * src[5] + tmp[10] * src[6];
+  dst[4] = tmp[1] * src[1] + tmp[2] * src[2] + tmp[5] * src[3];
+  dst[4] -= tmp[0] * src[1] + tmp[3] * src[2] + tmp[4] * src[3];
+  dst[5] = tmp[0] * src[0] + tmp[7] * src[2] + tmp[8] * src[3];
+  dst[5] -= tmp[1] * src[0] + tmp[6] * src[2] + tmp[9] * src[3];
+  dst[6] = tmp[3] * src[0] + tmp[6] * src[1] + tmp[11] * src[3];
+  dst[6] -= tmp[2] * src[0] + tmp[7] * src[1] + tmp[10] * src[3];
+  dst[7] = tmp[4] * src[0] + tmp[9] * src[1] + tmp[10] * src[2];
+  dst[7] -= tmp[5] * src[0] + tmp[8] * src[1] + tmp[11] * src[2];
+  tmp[0] = src[2] * src[7]; tmp[1] = src[3] * src[6]; tmp[2] = src[1] * src[7];
+  tmp[3] = src[3] * src[5]; tmp[4] = src[1] * src[6]; tmp[5] = src[2] * src[5];
+  tmp[6] = src[0] * src[7]; tmp[7] = src[3] * src[4]; tmp[8] = src[0] * src[6];
+  tmp[9] = src[2] * src[4]; tmp[10] = src[0] * src[5]; tmp[11] = src[1] * src[4];
+  dst[8] = tmp[0] * src[13] + tmp[3] * src[14] + tmp[4] * src[15];
+  dst[8] -= tmp[1] * src[13] + tmp[2] * src[14] + tmp[5] * src[15];
+  dst[9] = tmp[1] * src[12] + tmp[6] * src[14] + tmp[9] * src[15];
+  dst[9] -= tmp[0] * src[12] + tmp[7] * src[14] + tmp[8] * src[15];
+  dst[10] = tmp[2] * src[12] + tmp[7] * src[13] + tmp[10] * src[15];
+  dst[10] -= tmp[3] * src[12] + tmp[6] * src[13] + tmp[11] * src[15];
+  dst[11] = tmp[5] * src[12] + tmp[8] * src[13] + tmp[11] * src[14];
+  dst[11] -= tmp[4] * src[12] + tmp[9] * src[13] + tmp[10] * src[14];
+  dst[12] = tmp[2] * src[10] + tmp[5] * src[11] + tmp[1] * src[9];
+  dst[12] -= tmp[4] * src[11] + tmp[0] * src[9] + tmp[3] * src[10];
+  dst[13] = tmp[8] * src[11] + tmp[0] * src[8] + tmp[7] * src[10];
+  dst[13] -= tmp[6] * src[10] + tmp[9] * src[11] + tmp[1] * src[8];
+  dst[14] = tmp[6] * src[9] + tmp[11] * src[11] + tmp[3] * src[8];
+  dst[14] -= tmp[10] * src[11] + tmp[2] * src[8] + tmp[7] * src[9];
+  dst[15] = tmp[10] * src[10] + tmp[4] * src[8] + tmp[9] * src[9];
+  dst[15] -= tmp[8] * src[9] + tmp[11] * src[10] + tmp[5] * src[8];
+  double det = src[0] * dst[0] + src[1] * dst[1] + src[2] * dst[2] + src[3] * dst[3];
+  M4 r;  // identity-initialised, as `new myMatrix()`
+  if (std::fabs(det) > .0000001) {
+    for (int j = 0; j < 16; j++) dst[j] /= det;
+    for (int row = 0; row < 4; ++row) for (int col = 0; col < 4; ++col) r.m[row][col] = dst[4 * row + col];
+  }
+  return r;
+}
+// CTM array [glbl, inv, trans, adj] (DistRayTracer.java:399-405)
+struct CTM {
+  M4 g, inv, tr, adj;
+};
+static inline CTM build_ctm(const M4& g) {
+  CTM c;
+  c.g = g;
+  c.inv = invert(g);
+  c.tr = transpose(g);
+  c.adj = transpose(c.inv);
+  return c;
+}
+
+static inline V3 rot_around_axis(const V3& v1, const V3& u, double thet) {
+  double cT = std::cos(thet), sT = std::sin(thet), oneMC = 1 - cT, ux2 = u.x * u.x, uy2 = u.y * u.y,
+         uz2 = u.z * u.z, uxy = u.x * u.y, uxz = u.x * u.z, uyz = u.y * u.z, uzS = u.z * sT, uyS = u.y * sT,
+         uxS = u.x * sT, uxzC1 = uxz * oneMC, uxyC1 = uxy * oneMC, uyzC1 = uyz * oneMC;
+  return V3((ux2 * oneMC + cT) * v1.x + (uxyC1 - uzS) * v1.y + (uxzC1 + uyS) * v1.z,
+            (uxyC1 + uzS) * v1.x + (uy2 * oneMC + cT) * v1.y + (uyzC1 - uxS) * v1.z,
+            (uxzC1 - uyS) * v1.x + (uyzC1 + uxS) * v1.y + (uz2 * oneMC + cT) * v1.z);
+}
+static inline V3 ortho_vec(const V3& vec) {
+  V3 t(1, 1, 0);
+  normalize_ip(t);
+  if (std::fabs(dot(t, vec) - 1) < EPS) t = V3(0, 0, 1);
+  V3 r = cross(vec, t);
+  normalize_ip(r);
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// Keyed counter RNG replacing ThreadLocalRandom. Shared definition
+// with the product (DESIGN.md "RNG"); the product implements it independently.
+static inline uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+static inline uint64_t rng_bits(uint64_t seed, uint64_t a, uint32_t b, uint32_t c, uint32_t site, uint32_t k) {
+  uint64_t h = mix64(seed ^ mix64(a));
+  h = mix64(h ^ (((uint64_t)b << 32) | c));
+  h = mix64(h ^ (((uint64_t)site << 32) | k));
+  return h;
+}
+// JDK8 ThreadLocalRandom.nextDouble(origin, bound) mapping
+static inline double rng_range(uint64_t bits, double a, double b) {
+  double r = (double)(bits >> 11) * 0x1.0p-53;
+  r = r * (b - a) + a;
+  if (r >= b) {
+    int64_t ib;
+    std::memcpy(&ib, &b, 8);
+    ib -= 1;
+    std::memcpy(&r, &ib, 8);
+  }
+  return r;
+}
+
+// RNG draw sites (DESIGN.md "RNG")
+enum : uint32_t {
+  SITE_AA_Y = 1,
+  SITE_AA_X = 2,
+  SITE_DOF_ANG = 3,
+  SITE_DOF_RAD = 4,
+  SITE_TIME = 8,
+  SITE_DISK = 0x100,         // + light index, k = 0..3
+  SITE_SHADOW_TIME = 0x200,  // + light index, k = prim key
+  SITE_PH_DIR = 0x1000,      // photon emission, k = draw index
+  SITE_PH_BOUNCE = 0x1100,   // + bounce, k = draw index
+  SITE_PH_TIME = 0x1200,     // photon-path ray time, k = prim key
+};
+
+}  // namespace orc
