@@ -1,0 +1,58 @@
+"""Build libdistraytracer.so (HIP, gfx950) in-tree with hipcc.
+
+The shared library is the product: HIP kernels + host scene builder + C ABI
+(include/distraytracer.h). It is built in-tree so it travels to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+LIB_DIR = PKG / "lib"
+LIB_PATH = LIB_DIR / "libdistraytracer.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+SOURCES = ["trace.hip", "cli_loader.cpp", "scene_build.cpp", "photon.cpp"]
+HEADERS = ["rt_types.h", "rt_internal.h", "host_math.h", "trace_device.h"]
+# -ffp-contract=off: keep the reference's (Java) unfused double arithmetic so discrete
+# decisions (hits, shadows, TIR) match the oracle; no fast-math (IEEE Inf/NaN needed).
+COMPILE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
+                 "-Wall", "-Wno-unused-result", "-Wno-unused-function"]
+
+
+def _stale() -> bool:
+    if not LIB_PATH.exists():
+        return True
+    t = LIB_PATH.stat().st_mtime
+    deps = [CSRC / s for s in SOURCES + HEADERS] + [PKG.parent / "include" / "distraytracer.h"]
+    return any(p.stat().st_mtime > t for p in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    if not force and not _stale():
+        return LIB_PATH
+    LIB_DIR.mkdir(exist_ok=True)
+    tmp = LIB_PATH.with_suffix(".so.tmp%d" % os.getpid())
+    objs, logs = [], []
+    for src in SOURCES:  # .hip -> device+host; .cpp -> host-only C++ (no device pass)
+        obj = LIB_DIR / (src + ".o")
+        lang = [] if src.endswith(".hip") else ["-x", "c++"]
+        cmd = [HIPCC, *COMPILE_FLAGS, *lang, "-c", str(CSRC / src), "-o", str(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        logs.append(r.stderr)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n" + r.stderr[-4000:])
+        objs.append(str(obj))
+    r = subprocess.run([HIPCC, "-shared", "--offload-arch=gfx950", "-o", str(tmp), *objs], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("link failed:\n" + r.stderr[-4000:])
+    if verbose:
+        print("\n".join(logs))
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force=True))

@@ -1,0 +1,429 @@
+// Native mirror of the reference's `.cli` reader, myRTFileReader.readRTFile
+// (src/rayTracerDistAccelShdPhtnMap/myRTFileReader.java:15-349), and of the
+// builder state it drives in myScene (myScene.java:144-145 material state,
+// :305-324 accel lists, :413-444 lights, :447-521 prims, :1235-1323 matrix
+// stack). It emits the flattened rt_scene_desc that a JNI myScene subclass
+// would hand over, then calls rt_scene_create().
+//
+// Commands outside the hot-path scope (instances, sierpinski, wood/stone
+// textures, fisheye/ortho cameras) are rejected with RT_E_PARSE.
+#include <cctype>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/distraytracer.h"
+#include "host_math.h"
+#include "rt_internal.h"
+
+namespace rt {
+using namespace hm;
+
+namespace {
+
+struct Clr {
+  double r = 0, g = 0, b = 0;
+};
+static Clr clr(double r, double g, double b) { return Clr{jmin(1, r), jmin(1, g), jmin(1, b)}; }  // myColor clamp
+
+struct CliLoader {
+  std::string dir;
+  std::map<std::string, int> texIndex;
+  std::vector<Mat> stack{Mat::ident()};
+  // material state
+  Clr cDiff, cAmb, cSpec, permClr, kReflClr;
+  double phong = 0, kRefl = 0, kTrans = 0, rfrIdx = 0;
+  bool simple = false, txTop = false;
+  int txtrType = 0;
+  int texTop = -1;
+  double noiseScale = 1, turbMult = 1, colorScale = 10, colorMult = .2;
+  int octaves = 8;
+  D3 pdMult{10, 10, 10};
+  bool rndColors = false, useFwdTrans = false, useCustClrs = false;
+  Clr colors[2] = {clr(.7, .7, .7), clr(.2, .2, .2)};
+  bool photonMap = false, caustic = false;
+  // accumulated desc
+  std::vector<rt_prim_desc> prims;
+  std::vector<rt_material_desc> mats;
+  std::vector<rt_light_desc> lights;
+  std::vector<rt_accel_desc> accels;
+  std::vector<int32_t> members, top;
+  bool inList = false;
+  std::vector<int32_t> tmp;
+  rt_scene_desc d{};
+  int curRpp = 0;
+  std::string err;
+
+  void put_ctm(double* dst) { std::memcpy(dst, stack.back().m, sizeof(double) * 16); }
+  void set_surface(Clr df, Clr am, Clr sp, double ph, double kr) {  // myScene.setSurface :817-828
+    txtrType = 0;
+    cDiff = df; cAmb = am; cSpec = sp; phong = ph;
+    kRefl = kr; kReflClr = clr(kr, kr, kr);
+    rfrIdx = 0; permClr = clr(0, 0, 0); kTrans = 0;
+  }
+  int material() {  // getCurShader (myScene.java:524-542): a fresh shader per object, dedup by value
+    rt_material_desc m;
+    std::memset(&m, 0, sizeof(m));
+    m.simple = simple;
+    m.texture = (txtrType == 1 || txtrType == 2 || txtrType == 4) ? txtrType : RT_TEX_NONE;
+    m.tex_top = (txtrType == 1 && txTop) ? texTop : -1;
+    m.use_photon_map = photonMap;
+    m.caustic_photons = caustic;
+    m.diffuse[0] = cDiff.r; m.diffuse[1] = cDiff.g; m.diffuse[2] = cDiff.b;
+    m.ambient[0] = cAmb.r; m.ambient[1] = cAmb.g; m.ambient[2] = cAmb.b;
+    m.specular[0] = cSpec.r; m.specular[1] = cSpec.g; m.specular[2] = cSpec.b;
+    m.phong_exp = phong;
+    m.k_refl = kRefl;
+    m.k_refl_clr[0] = kReflClr.r; m.k_refl_clr[1] = kReflClr.g; m.k_refl_clr[2] = kReflClr.b;
+    m.k_trans = kTrans;
+    m.perm = rfrIdx;
+    m.perm_clr[0] = permClr.r; m.perm_clr[1] = permClr.g; m.perm_clr[2] = permClr.b;
+    if (txtrType == 2 || txtrType == 4) {
+      m.noise_scale = noiseScale; m.turb_mult = turbMult; m.color_scale = colorScale; m.color_mult = colorMult;
+      m.period_mult[0] = pdMult.x; m.period_mult[1] = pdMult.y; m.period_mult[2] = pdMult.z;
+      m.octaves = octaves; m.rnd_colors = rndColors; m.use_fwd_trans = useFwdTrans;
+      for (int i = 0; i < 2; ++i) { m.colors[i][0] = colors[i].r; m.colors[i][1] = colors[i].g; m.colors[i][2] = colors[i].b; }
+    }
+    for (size_t i = 0; i < mats.size(); ++i)
+      if (std::memcmp(&mats[i], &m, sizeof(m)) == 0) return (int)i;
+    mats.push_back(m);
+    return (int)mats.size() - 1;
+  }
+  void add_prim(rt_prim_desc& p) {  // addObjectToScene (myScene.java:558-565)
+    p.material = material();
+    int idx = (int)prims.size();
+    prims.push_back(p);
+    if (inList) tmp.push_back(idx);
+    else top.push_back(idx);
+  }
+  rt_prim_desc new_prim(int type) {
+    rt_prim_desc p;
+    std::memset(&p, 0, sizeof(p));
+    p.type = type;
+    put_ctm(p.ctm);
+    return p;
+  }
+  void reset_dflt_txtr() {  // resetDfltTxtrVals (myScene.java:579-586)
+    txtrType = 0; octaves = 4; rndColors = false; useCustClrs = false; useFwdTrans = false;
+    noiseScale = 1.0; turbMult = 1.0; colorScale = 5.0; colorMult = .1;
+    pdMult = d3(1.0, 1.0, 1.0);
+    colors[0] = clr(0.05, 0.05, 0.05); colors[1] = clr(1.0, 1.0, 1.0);
+  }
+  static double num(const std::vector<std::string>& t, size_t i) {
+    if (i >= t.size()) throw std::out_of_range("missing argument");
+    return std::stod(t[i]);
+  }
+  bool read_perlin(const std::vector<std::string>& v) {  // readProcTxtrPerlinVals (myScene.java:642-672)
+    try {
+      if (v.size() < 11) return true;
+      noiseScale = num(v, 1); octaves = std::stoi(v.at(2)); turbMult = num(v, 3);
+      pdMult = d3(num(v, 4), num(v, 5), num(v, 6));
+      D3 py = d3(num(v, 7), num(v, 8), num(v, 9));
+      if (((py.x * py.x) + (py.y * py.y)) + (py.z * py.z) > 0) {
+        py = d3(py.x * (TWO_PI_F - 1.0), py.y * (TWO_PI_F - 1.0), py.z * (TWO_PI_F - 1.0));
+        py = d3(py.x + 1.0, py.y + 1.0, py.z + 1.0);
+        pdMult = d3(pdMult.x * py.x, pdMult.y * py.y, pdMult.z * py.z);
+      }
+      useFwdTrans = (num(v, 10) == 1.0);
+      if (v.size() >= 13) {
+        colorScale = num(v, 11); colorMult = num(v, 12); rndColors = true;
+      } else {
+        rndColors = false; colorScale = 25.0; colorMult = .1;
+      }
+      return false;
+    } catch (...) {
+      return true;
+    }
+  }
+
+  bool read(const std::string& fname, bool isMain) {
+    std::ifstream f(dir + "/" + fname);
+    if (!f) { err = "cannot open " + dir + "/" + fname; return false; }
+    std::string line;
+    rt_prim_desc poly;
+    bool inPoly = false;
+    int vc = 0;
+    while (std::getline(f, line)) {
+      std::vector<std::string> t;
+      {  // PApplet.splitTokens(line, " ")
+        std::string cur;
+        for (char ch : line) {
+          if (ch == ' ' || ch == '\t' || ch == '\r') { if (!cur.empty()) { t.push_back(cur); cur.clear(); } }
+          else cur.push_back(ch);
+        }
+        if (!cur.empty()) t.push_back(cur);
+      }
+      if (t.empty() || t[0][0] == '#') continue;
+      const std::string& c = t[0];
+      try {
+        if (c == "fov") {  // :51-58
+          if (!isMain) continue;
+          d.rays_per_pixel = (curRpp != 0) ? curRpp : 1;
+          d.fov = num(t, 1);
+        } else if (c == "lens") {
+          d.dof = 1; d.lens_radius = num(t, 1); d.lens_focal = num(t, 2);
+        } else if (c == "write") {
+          break;  // the reference renders here (:86-93)
+        } else if (c == "read") {
+          if (!read(t.at(1), false)) return false;
+        } else if (c == "rays_per_pixel") {
+          curRpp = std::stoi(t.at(1)); d.rays_per_pixel = curRpp;
+        } else if (c == "antialias") {
+          curRpp = std::stoi(t.at(1)) * std::stoi(t.at(2)); d.rays_per_pixel = curRpp;
+        } else if (c == "background") {  // :129-148
+          if (t.at(1) == "texture") {
+            auto it = texIndex.find(t.at(2));
+            if (it == texIndex.end()) { err = "texture not registered: " + t.at(2); return false; }
+            d.bkg_texture = it->second;
+            d.skydome[0] = num(t, 3); d.skydome[1] = num(t, 4); d.skydome[2] = num(t, 5); d.skydome[3] = num(t, 6);
+          } else {
+            Clr b = clr(num(t, 1), num(t, 2), num(t, 3));
+            d.background[0] = b.r; d.background[1] = b.g; d.background[2] = b.b;
+            txtrType = 0;
+          }
+        } else if (c == "point_light" || c == "spotlight" || c == "disk_light") {  // myScene.java:413-444
+          if (inList) { err = "light inside accel list unsupported"; return false; }
+          rt_light_desc L;
+          std::memset(&L, 0, sizeof(L));
+          put_ctm(L.ctm);
+          L.pos[0] = num(t, 1); L.pos[1] = num(t, 2); L.pos[2] = num(t, 3);
+          Clr col;
+          if (c == "point_light") {
+            L.type = RT_LIGHT_POINT;
+            col = clr(num(t, 4), num(t, 5), num(t, 6));
+          } else if (c == "spotlight") {
+            L.type = RT_LIGHT_SPOT;
+            L.dir[0] = num(t, 4); L.dir[1] = num(t, 5); L.dir[2] = num(t, 6);
+            L.inner_deg = num(t, 7); L.outer_deg = num(t, 8);
+            col = clr(num(t, 9), num(t, 10), num(t, 11));
+          } else {
+            L.type = RT_LIGHT_DISK;
+            L.radius = num(t, 4);
+            L.dir[0] = num(t, 5); L.dir[1] = num(t, 6); L.dir[2] = num(t, 7);
+            col = clr(num(t, 8), num(t, 9), num(t, 10));
+          }
+          L.color[0] = col.r; L.color[1] = col.g; L.color[2] = col.b;
+          lights.push_back(L);
+        } else if (c == "caustic_photons" || c == "diffuse_photons") {  // setPhotonHandling :919-931
+          photonMap = true;
+          caustic = (c.find("caustic") != std::string::npos);
+          d.photon_mode = caustic ? 2 : 1;
+          d.photon_count = std::stoi(t.at(1));
+          d.photon_k = std::stoi(t.at(2));
+          d.photon_max_dist = (double)std::stof(t.at(3));
+        } else if (c == "final_gather") {
+        } else if (c == "diffuse" || c == "reflective") {
+          txTop = false;
+          set_surface(clr(num(t, 1), num(t, 2), num(t, 3)), clr(num(t, 4), num(t, 5), num(t, 6)), clr(0, 0, 0), 0,
+                      c == "reflective" ? num(t, 7) : 0);
+        } else if (c == "shiny" || c == "surface") {  // setSurfaceShiny (myRTFileReader.java:358-378)
+          Clr df = clr(num(t, 1), num(t, 2), num(t, 3)), am = clr(num(t, 4), num(t, 5), num(t, 6)),
+              sp = clr(num(t, 7), num(t, 8), num(t, 9));
+          double ph = num(t, 10), kr = num(t, 11), kt = 0, ri = 0;
+          txTop = false;
+          set_surface(df, am, sp, ph, kr);
+          if (t.size() > 12) {
+            kt = num(t, 12);
+            kTrans = kt;
+            if (t.size() > 13) {
+              ri = num(t, 13);
+              rfrIdx = ri; permClr = clr(ri, ri, ri);
+              if (t.size() > 16) permClr = clr(num(t, 14), num(t, 15), num(t, 16));
+            }
+          }
+          if (c == "shiny" && ((kt > 0) || (ri > 0))) simple = true;
+        } else if (c == "perm") {
+          rfrIdx = num(t, 1); permClr = clr(rfrIdx, rfrIdx, rfrIdx);
+          if (t.size() > 4) permClr = clr(num(t, 2), num(t, 3), num(t, 4));
+        } else if (c == "phong") { phong = num(t, 1);
+        } else if (c == "krefl") { kRefl = num(t, 1); kReflClr = clr(kRefl, kRefl, kRefl);
+        } else if (c == "ktrans") { kTrans = num(t, 1);
+        } else if (c == "depth") {
+        } else if (c == "begin_list") {
+          inList = true; tmp.clear();
+        } else if (c == "end_list" || c == "end_accel") {  // endTmpObjList (myScene.java:305-324)
+          inList = false;
+          rt_accel_desc a;
+          std::memset(&a, 0, sizeof(a));
+          a.type = (c == "end_accel") ? 1 : 0;
+          a.first = (int)members.size();
+          a.count = (int)tmp.size();
+          put_ctm(a.ctm);
+          members.insert(members.end(), tmp.begin(), tmp.end());
+          top.push_back(~(int32_t)accels.size());
+          accels.push_back(a);
+          tmp.clear();
+        } else if (c == "texture" || c == "image_texture") {  // :257-273
+          std::string lo = t.at(1);
+          for (auto& ch : lo) ch = (char)std::tolower(ch);
+          if (lo == "top" || lo != "bottom") {
+            std::string name = (lo == "top") ? t.at(2) : t.at(1);
+            auto it = texIndex.find(name);
+            if (it == texIndex.end()) { err = "texture not registered: " + name; return false; }
+            texTop = it->second;
+            txTop = true;
+          }
+          txtrType = 1;
+        } else if (c == "noise") {
+          reset_dflt_txtr(); txtrType = 2; noiseScale = num(t, 1);
+        } else if (c == "marble") {  // setTexture (myScene.java:743-755)
+          reset_dflt_txtr();
+          txtrType = 4;
+          bool dflt = read_perlin(t);
+          if (!useCustClrs) { colors[0] = clr(0.05, 0.05, 0.05); colors[1] = clr(0.95, 0.98, 0.92); }
+          if (dflt) {
+            octaves = 16; rndColors = true; useFwdTrans = false;
+            noiseScale = 1.0; turbMult = 15.0; colorScale = 24.0; colorMult = .1;
+            pdMult = d3(TWO_PI_F * 0.1, TWO_PI_F * 31.4, TWO_PI_F * 4.1);
+          }
+        } else if (c == "begin") {  // :290-295
+          poly = new_prim((t.size() > 1 && t[1] == "quad") ? RT_PRIM_QUAD : RT_PRIM_TRIANGLE);
+          poly.nverts = poly.type == RT_PRIM_QUAD ? 4 : 3;
+          inPoly = true;
+          vc = 0;
+        } else if (c == "texture_coord") {
+          if (!inPoly || vc >= poly.nverts) throw std::out_of_range("texture_coord outside polygon");
+          poly.uv[vc][0] = num(t, 1); poly.uv[vc][1] = num(t, 2);
+        } else if (c == "vertex") {
+          if (!inPoly || vc >= poly.nverts) throw std::out_of_range("vertex outside polygon");
+          poly.v[vc][0] = num(t, 1); poly.v[vc][1] = num(t, 2); poly.v[vc][2] = num(t, 3);
+          vc++;
+        } else if (c == "end") {
+          if (!inPoly) throw std::out_of_range("end without begin");
+          add_prim(poly);
+          inPoly = false;
+        } else if (c == "sphere" || c == "sphereIn" || c == "moving_sphere" || c == "ellipsoid") {
+          rt_prim_desc p = new_prim(c == "moving_sphere" ? RT_PRIM_MOVING_SPHERE : RT_PRIM_SPHERE);
+          if (c == "ellipsoid") {
+            p.p[3] = num(t, 1); p.p[4] = num(t, 2); p.p[5] = num(t, 3);
+            p.p[0] = num(t, 4); p.p[1] = num(t, 5); p.p[2] = num(t, 6);
+          } else {
+            p.p[3] = p.p[4] = p.p[5] = num(t, 1);
+            p.p[0] = num(t, 2); p.p[1] = num(t, 3); p.p[2] = num(t, 4);
+          }
+          if (c == "moving_sphere") { p.p[6] = num(t, 5); p.p[7] = num(t, 6); p.p[8] = num(t, 7); }
+          if (c == "sphereIn") p.flags |= RT_PRIM_INVERTED;
+          add_prim(p);
+        } else if (c == "cyl" || c == "cylinder" || c == "hollow_cylinder") {
+          rt_prim_desc p = new_prim(c == "hollow_cylinder" ? RT_PRIM_HOLLOW_CYLINDER : RT_PRIM_CYLINDER);
+          double ox = 0, oy = 1, oz = 0;
+          if (c == "cyl") {
+            p.p[0] = num(t, 1); p.p[1] = num(t, 2); p.p[2] = num(t, 3); p.p[3] = num(t, 4); p.p[4] = num(t, 5);
+            if (t.size() > 8) { ox = num(t, 6); oy = num(t, 7); oz = num(t, 8); }
+          } else {  // cylinder radius x z ymin ymax
+            p.p[0] = num(t, 1); p.p[2] = num(t, 2); p.p[4] = num(t, 3); p.p[3] = num(t, 4);
+            p.p[1] = num(t, 5) - p.p[3];
+          }
+          p.p[5] = ox; p.p[6] = oy; p.p[7] = oz;
+          add_prim(p);
+        } else if (c == "box") {
+          rt_prim_desc p = new_prim(RT_PRIM_BOX);
+          for (int i = 0; i < 6; ++i) p.p[i] = num(t, 1 + i);
+          add_prim(p);
+        } else if (c == "plane") {
+          rt_prim_desc p = new_prim(RT_PRIM_PLANE);
+          for (int i = 0; i < 4; ++i) p.p[i] = num(t, 1 + i);
+          p.nverts = 4;
+          add_prim(p);
+        } else if (c == "push") {  // gtPushMatrix :1241-1246
+          stack.push_back(stack.back());
+        } else if (c == "pop") {
+          if (stack.size() > 1) stack.pop_back();
+        } else if (c == "translate") {  // :1256-1264
+          Mat T = Mat::ident();
+          T.m[3] = num(t, 1); T.m[7] = num(t, 2); T.m[11] = num(t, 3);
+          stack.back() = mul(stack.back(), T);
+        } else if (c == "scale") {
+          Mat S = Mat::ident();
+          S.m[0] = num(t, 1); S.m[5] = num(t, 2); S.m[10] = num(t, 3);
+          stack.back() = mul(stack.back(), S);
+        } else if (c == "rotate") {  // gtRotate :1280-1318
+          double ang = num(t, 1), ax = num(t, 2), ay = num(t, 3), az = num(t, 4);
+          double ar = (double)(ang * M_PI) / 180.0;
+          D3 av = normalized(d3(ax, ay, az));
+          D3 nv = (ax == 0) ? d3(1, 0, 0) : d3(0, 1, 0);
+          D3 bv = normalized(cross(av, nv));
+          D3 cv = normalized(cross(av, bv));
+          Mat R1 = Mat::ident(), R2 = Mat::ident();
+          R1.m[0] = av.x; R1.m[1] = av.y; R1.m[2] = av.z;
+          R1.m[4] = bv.x; R1.m[5] = bv.y; R1.m[6] = bv.z;
+          R1.m[8] = cv.x; R1.m[9] = cv.y; R1.m[10] = cv.z;
+          R2.m[5] = std::cos(ar); R2.m[6] = -std::sin(ar); R2.m[9] = std::sin(ar); R2.m[10] = std::cos(ar);
+          stack.back() = mul(stack.back(), mul(transpose(R1), mul(R2, R1)));
+        } else if (c == "reset_timer" || c == "print_timer" || c == "refine") {
+          // timers and progressive `refine` are outside the kernel path (documented override)
+        } else {
+          err = "unsupported command '" + c + "' in " + fname;
+          return false;
+        }
+      } catch (const std::exception& e) {
+        err = "parse error in " + fname + " at '" + c + "': " + e.what();
+        return false;
+      }
+    }
+    return true;
+  }
+};
+
+}  // namespace
+
+}  // namespace rt
+
+using namespace rt;
+
+static int load_desc(const char* scene_dir, const char* cli_file, int num_textures, const char* const* texture_names,
+                     const rt_texture_desc* textures, CliLoader& L) {
+  if (!scene_dir || !cli_file || (num_textures > 0 && (!texture_names || !textures)))
+    return set_error(RT_E_INVALID, "rt_scene_load_cli: null argument");
+  L.dir = scene_dir;
+  std::memset(&L.d, 0, sizeof(L.d));
+  L.d.fov = 60;  // default FOV scene (myRTFileReader.java:27-28)
+  L.d.bkg_texture = -1;
+  for (int i = 0; i < num_textures; ++i) L.texIndex[texture_names[i]] = i;
+  if (!L.read(cli_file, true)) {
+    bool io = L.err.rfind("cannot open", 0) == 0;
+    return set_error(io ? RT_E_IO : RT_E_PARSE, L.err);
+  }
+  rt_scene_desc& d = L.d;
+  d.num_prims = (int)L.prims.size(); d.prims = L.prims.data();
+  d.num_materials = (int)L.mats.size(); d.materials = L.mats.data();
+  d.num_lights = (int)L.lights.size(); d.lights = L.lights.data();
+  d.num_accels = (int)L.accels.size(); d.accels = L.accels.data(); d.accel_members = L.members.data();
+  d.num_top = (int)L.top.size(); d.top = L.top.data();
+  d.num_textures = num_textures; d.textures = textures;
+  return RT_OK;
+}
+
+extern "C" int rt_scene_load_cli(const char* scene_dir, const char* cli_file, int num_textures,
+                                 const char* const* texture_names, const rt_texture_desc* textures, int device,
+                                 rt_scene** out) {
+  if (!out) return set_error(RT_E_INVALID, "rt_scene_load_cli: null out");
+  CliLoader L;
+  int rc = load_desc(scene_dir, cli_file, num_textures, texture_names, textures, L);
+  if (rc) return rc;
+  return rt_scene_create(&L.d, device, out);
+}
+
+// Host-only: parse + build the flattened scene without touching a device, report the
+// rt_scene_info fields (device bytes = host layout bytes). Used by the CPU test suite.
+extern "C" int rt_scene_inspect_cli(const char* scene_dir, const char* cli_file, int num_textures,
+                                    const char* const* texture_names, const rt_texture_desc* textures, int64_t* info,
+                                    int n) {
+  if (!info) return set_error(RT_E_INVALID, "null info");
+  CliLoader L;
+  int rc = load_desc(scene_dir, cli_file, num_textures, texture_names, textures, L);
+  if (rc) return rc;
+  HostScene hs;
+  rc = build_host_scene(&L.d, hs);
+  if (rc) return rc;
+  int64_t bytes = (int64_t)(hs.xf.size() * sizeof(XformD) + hs.tri.size() * sizeof(TriD) + hs.prim.size() * sizeof(PrimD) +
+                            hs.node.size() * sizeof(NodeD) + hs.leaf.size() * sizeof(LeafD) + hs.member.size() * 4 +
+                            hs.accel.size() * sizeof(AccelD) + hs.top.size() * sizeof(TopD) + hs.mat.size() * sizeof(MatD) +
+                            hs.light.size() * sizeof(LightD) + hs.texel.size() * 4);
+  int64_t v[12] = {(int64_t)hs.top.size(), (int64_t)hs.light.size(), hs.bvhInternal, hs.bvhLeaves, hs.bvhDepth,
+                   hs.bvhPrims, hs.nprims, hs.rpp, bytes, (int64_t)hs.tri.size(), 0, (int64_t)hs.mat.size()};
+  for (int i = 0; i < n && i < 12; ++i) info[i] = v[i];
+  return RT_OK;
+}

@@ -1,0 +1,56 @@
+// Internal host-side declarations shared by the loader, builder and HIP launch code.
+#pragma once
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/distraytracer.h"
+#include "rt_types.h"
+
+namespace rt {
+
+int set_error(int code, const std::string& msg);
+
+// Flattened scene on the host (mirrors SceneD) -- built by scene_build.cpp.
+struct HostScene {
+  std::vector<XformD> xf;
+  std::vector<TriD> tri;
+  std::vector<PrimD> prim;
+  std::vector<NodeD> node;
+  std::vector<LeafD> leaf;
+  std::vector<int32_t> member;
+  std::vector<AccelD> accel;
+  std::vector<TopD> top;
+  std::vector<MatD> mat;
+  std::vector<LightD> light;
+  std::vector<TexD> tex;
+  std::vector<uint32_t> texel;
+  std::vector<PhotonD> photon;
+  int photonRoot = -1;
+  // scene parameters
+  double fov = 60;
+  double bg[3] = {0, 0, 0};
+  int bkgTex = -1;
+  double sky[4] = {0, 0, 0, 0};
+  int dof = 0;
+  double lensRadius = 0, lensFocal = 0;
+  int rpp = 0;
+  int photonMode = 0, photonCount = 0, photonK = 0;
+  double photonMaxD2 = 0;
+  // statistics (compare with the oracle's builder)
+  int64_t bvhInternal = 0, bvhLeaves = 0, bvhDepth = 0, bvhPrims = 0, nprims = 0;
+};
+
+int build_host_scene(const rt_scene_desc* d, HostScene& hs);  // scene_build.cpp
+
+}  // namespace rt
+
+struct rt_scene {
+  rt::HostScene hs;
+  int device = 0;
+  rt::SceneD dev{};
+  std::vector<void*> allocs;
+  size_t devBytes = 0;
+  bool photonsUploaded = false;
+  void* counters = nullptr;  // device uint64[RT_ST_N]
+};

@@ -1,0 +1,139 @@
+// Flattened scene layout in HBM (host builder <-> HIP kernels).
+// DESIGN.md "Data layout in HBM" documents every record and its byte size.
+#pragma once
+#include <stdint.h>
+
+namespace rt {
+
+// Per distinct CTM (deduplicated by value): forward, inverse (myMatrix.InvertMe
+// cofactor algorithm, myVector.java:111-196) and adjoint = inverse^T
+// (DistRayTracer.java:399-405). 384 B.
+struct XformD {
+  double g[16];
+  double inv[16];
+  double adj[16];
+};
+
+// Triangle, 128 B: vertices in object space, file order; orientation A normal
+// (orientation B is exactly -n); plane D for both
+// orientations (setEQ uses the current first vertex, myPlanarObject.java:90).
+struct TriD {
+  double v[3][3];
+  double n[3];
+  double dA, dB;
+  int32_t xf;   // own CTM
+  int32_t xfc;  // accel CTM x own CTM (reCalcCTMHitNorm, Q4), -1 at top level
+  int32_t mat;
+  uint32_t key; // creation index (RNG prim key)
+};
+
+enum : int32_t {
+  PT_TRI = 0, PT_QUAD = 1, PT_PLANE = 2, PT_SPHERE = 3, PT_MSPHERE = 4, PT_CYL = 5, PT_HCYL = 6, PT_BOX = 7
+};
+
+// Every other primitive, 256 B. Field use by type:
+//  QUAD/PLANE: a[0..11] v[4][3], a[12..14] NA, a[15..17] NB, a[18] DA, a[19] DB, a[20..27] uv[4][2]
+//  SPHERE/MSPHERE: a[0..2] origin (origin0), a[3..5] radii, a[6..8] origin1
+//  CYL/HCYL: a[0..2] origin, a[3] radX, a[4] radZ, a[5] height, a[6] yTop, a[7] yBottom, a[8..15] caps
+//  BOX: a[0..2] min, a[3..5] max
+struct PrimD {
+  int32_t type, xf, xfc, mat;
+  uint32_t key;
+  int32_t flags;  // bit0 inverted (sphereIn)
+  int32_t pad[2];
+  double a[28];
+};
+
+// BVH node with both child boxes (reference topology, myBVH.addObjList
+// myGeomBase.java:360-386). child >= 0: node index; child < 0: leaf ~index. 128 B.
+struct NodeD {
+  double lmin[3], lmax[3], rmin[3], rmax[3];
+  int32_t left, right;
+  int32_t pad[6];
+};
+struct LeafD {
+  int32_t start, count;  // range in leaf member refs (>= 0 tri index, < 0 ~prim index)
+};
+// A myBVH or a myGeomList (one leaf holding the whole list).
+struct AccelD {
+  double bmin[3], bmax[3];  // root box (list box / BVH root box)
+  int32_t xf;
+  int32_t root;      // child ref: >= 0 node, < 0 ~leaf
+  int32_t is_list;   // end_list
+  int32_t pad;
+};
+enum : int32_t { TOP_TRI = 0, TOP_PRIM = 1, TOP_ACCEL = 2 };
+struct TopD {
+  int32_t kind, idx, xf;
+  uint32_t key;
+};
+
+struct MatD {
+  double diffuse[3], ambient[3], specular[3];
+  double kreflclr[3], permclr[3];
+  double phtnDiffScl[3], phtnPermClr[3];
+  double phong, krefl, ktrans, perm, diffConst, avgDiffClr;
+  // noise / marble
+  double scale, turbMult, colorScale, colorMult, pmMag;
+  double periodMult[3];
+  double colors[2][3];
+  int32_t simple, hasCaustic, usePhotonMap, isCausticPhtn;
+  int32_t tex, texTop, octaves, rndColors;
+  int32_t useFwdTrans, pad[3];
+};
+
+struct LightD {
+  int32_t type, index, pad[2];
+  double origin[3];   // object space (getOrigin)
+  double color[3];    // clamped <= 1
+  double orient[3];   // normalized
+  double tangent[3];  // disk surfTangent / spot oPhAxis
+  double innerRad, outerRad, radDiff, radius;
+  double g[16];       // light CTM (forward)
+};
+
+struct TexD {
+  int32_t w, h;
+  int64_t off;  // offset into the texel buffer (uint32 0xAARRGGBB)
+};
+
+// photon kd-tree node (myKD_Node + myPhoton, myLight.java:278-298), 64 B
+struct PhotonD {
+  double pos[3];
+  double pwr[3];
+  int32_t axis, left, right, pad;
+};
+
+// device-side scene handle (all pointers are device pointers)
+struct SceneD {
+  const XformD* xf;
+  const TriD* tri;
+  const PrimD* prim;
+  const NodeD* node;
+  const LeafD* leaf;
+  const int32_t* member;
+  const AccelD* accel;
+  const TopD* top;
+  const MatD* mat;
+  const LightD* light;
+  const TexD* tex;
+  const uint32_t* texel;
+  const PhotonD* photon;
+  int32_t ntop, nlight, nphoton, photonRoot;
+  int32_t photonK;
+  double photonMaxD2;
+  double bg[3];
+  int32_t bkgTex;
+  double sky[4];
+  int32_t dof;
+  double lensRadius, lensFocal;
+  int32_t numRays;  // recursion budget (myScene.numRays = 8)
+};
+
+struct ParamsD {
+  int32_t W, H, spp, row0, nrows, rowStep;
+  uint64_t seed;
+  double viewZ;
+};
+
+}  // namespace rt

@@ -1,0 +1,315 @@
+// Device-side trace loop for gfx950 (included by trace.hip only).
+//
+// One lane = one pixel; its samples are traced sequentially so the per-pixel
+// sum keeps the reference's accumulation order (myScene.java:1451-1460).
+// Geometry and shading are IEEE fp64 with the reference's expression order
+// (compiled -ffp-contract=off, no fast-math) so that every discrete decision
+// (hit object, shadow, TIR) matches the oracle; see DESIGN.md "Precision".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_types.h"
+
+namespace rt {
+namespace dv {
+
+#define DEVI __device__ __forceinline__
+
+static constexpr double EPS = 0.0000001;
+static constexpr double DMAX = 1.7976931348623157e308;
+static constexpr double TWO_PI_F = 6.2831854820251465;   // (double)PConstants.TWO_PI
+static constexpr double PI_F = 3.1415927410125732;       // (double)PConstants.PI
+static constexpr double PI_D = 3.141592653589793;        // Math.PI
+
+enum : uint32_t {
+  SITE_AA_Y = 1, SITE_AA_X = 2, SITE_DOF_ANG = 3, SITE_DOF_RAD = 4, SITE_TIME = 8,
+  SITE_DISK = 0x100, SITE_SHADOW_TIME = 0x200
+};
+enum { C_CAMERA = 0, C_SHADOW, C_REFL, C_REFR, C_BOX, C_TRI, C_QUAD, C_IMPLICIT, C_LIGHT, C_PHOTON, C_TEXEL,
+       C_NODE, C_LEAF, C_MEMBER, C_ROOT, C_N = 16 };
+
+struct V {
+  double x, y, z;
+};
+DEVI V mk(double x, double y, double z) { V r; r.x = x; r.y = y; r.z = z; return r; }
+DEVI V sub(V a, V b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+DEVI V add(V a, V b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+DEVI V scl(V a, double s) { return mk(a.x * s, a.y * s, a.z * s); }
+DEVI double dot(V a, V b) { return ((a.x * b.x) + (a.y * b.y)) + (a.z * b.z); }
+DEVI V cross(V a, V b) { return mk((a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x)); }
+DEVI double mag(V a) { return sqrt(((a.x * a.x) + (a.y * a.y)) + (a.z * a.z)); }
+DEVI V nrmz(V a) {  // myVector._normalize: division, no-op on zero
+  double m = mag(a);
+  if (m == 0) return a;
+  return mk(a.x / m, a.y / m, a.z / m);
+}
+DEVI bool veq(V a, V b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
+DEVI V ld3(const double* p) { return mk(p[0], p[1], p[2]); }
+DEVI double jmin(double a, double b) { return (a != a) ? a : ((a <= b) ? a : b); }  // Math.min (finite paths)
+DEVI double jmax(double a, double b) { return (a != a) ? a : ((a >= b) ? a : b); }
+DEVI int32_t jd2i(double v) {
+  if (v != v) return 0;
+  if (v >= 2147483647.0) return 2147483647;
+  if (v <= -2147483648.0) return (int32_t)0x80000000;
+  return (int32_t)v;
+}
+// myMatrix.multVert: accumulate from 0 in column order (keeps signed-zero behaviour)
+DEVI V xpt(const double* m, V p) {
+  double r[3];
+#pragma unroll
+  for (int row = 0; row < 3; ++row) {
+    double a = 0.0;
+    a += m[row * 4 + 0] * p.x;
+    a += m[row * 4 + 1] * p.y;
+    a += m[row * 4 + 2] * p.z;
+    a += m[row * 4 + 3] * 1.0;
+    r[row] = a;
+  }
+  return mk(r[0], r[1], r[2]);
+}
+DEVI V xvec(const double* m, V p) {
+  double r[3];
+#pragma unroll
+  for (int row = 0; row < 3; ++row) {
+    double a = 0.0;
+    a += m[row * 4 + 0] * p.x;
+    a += m[row * 4 + 1] * p.y;
+    a += m[row * 4 + 2] * p.z;
+    a += m[row * 4 + 3] * 0.0;
+    r[row] = a;
+  }
+  return mk(r[0], r[1], r[2]);
+}
+
+// keyed counter RNG (same definition as the oracle's; DESIGN.md "RNG")
+DEVI uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+DEVI double rng(uint64_t seed, uint64_t a, uint32_t b, uint32_t c, uint32_t site, uint32_t k, double lo, double hi) {
+  uint64_t h = mix64(seed ^ mix64(a));
+  h = mix64(h ^ (((uint64_t)b << 32) | c));
+  h = mix64(h ^ (((uint64_t)site << 32) | k));
+  double r = (double)(h >> 11) * 0x1.0p-53;
+  r = r * (hi - lo) + lo;
+  if (r >= hi) r = __longlong_as_double(__double_as_longlong(hi) - 1);
+  return r;
+}
+
+// RNG key of the ray currently traced
+struct Key {
+  uint64_t seed, pixel;
+  uint32_t sample, node;
+};
+
+// World ray with the reference's in-place re-normalisation state
+// (myRay.getTransformedRay normalises the source direction, myRay.java:91-93).
+struct WRay {
+  V o, d;
+  bool stable;  // normalize(d) == d
+  bool moved;   // d changed since the cached accel-space ray was built
+};
+DEVI void renorm(WRay& r) {
+  if (!r.stable) {
+    V n = nrmz(r.d);
+    r.stable = veq(n, r.d);
+    if (!r.stable) r.moved = true;
+    r.d = n;
+  }
+}
+
+struct Counters {
+  uint64_t c[C_N];
+};
+
+// ---------------------------------------------------------------------------
+// primitive tests (object space). `args` carries what the hit record needs:
+// planar orientation, cylinder face, box plane.
+DEVI bool slab(const double* mn, const double* mx, V o, V d, double& tEntry) {  // myBBox.intersectCheck :132-162
+  double ro[3] = {o.x, o.y, o.z}, rd[3] = {d.x, d.y, d.z};
+  double tMin[3], tMax[3];
+  double biggestMin = -DMAX;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    double t1 = (mn[i] - ro[i]) / rd[i];
+    double t2 = (mx[i] - ro[i]) / rd[i];
+    if (t1 < t2) {
+      tMin[i] = t1; tMax[i] = t2;
+      if (biggestMin < t1) biggestMin = t1;
+    } else {
+      tMin[i] = t2; tMax[i] = t1;
+      if (biggestMin < t2) biggestMin = t2;
+    }
+  }
+  double mnv = DMAX, mxv = -DMAX;  // p.min / p.max skip NaN
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (tMax[i] < mnv) mnv = tMax[i];
+    if (tMin[i] > mxv) mxv = tMin[i];
+  }
+  tEntry = biggestMin;
+  return (mnv > mxv) && biggestMin > 0;
+}
+DEVI int slab_plane(const double* mn, const double* mx, V o, V d) {  // plane idx for myBBox normals
+  double ro[3] = {o.x, o.y, o.z}, rd[3] = {d.x, d.y, d.z};
+  double biggestMin = -DMAX;
+  int idx = -1;
+  for (int i = 0; i < 3; ++i) {
+    double t1 = (mn[i] - ro[i]) / rd[i], t2 = (mx[i] - ro[i]) / rd[i];
+    if (t1 < t2) { if (biggestMin < t1) { idx = i; biggestMin = t1; } }
+    else { if (biggestMin < t2) { idx = i + 3; biggestMin = t2; } }
+  }
+  return idx;
+}
+
+// planar: orientation with N.d < 0 (the reference flips the vertex order in place, Q5)
+template <int NV, bool PLANE>
+DEVI bool planar_test(const double (*v)[3], V nA, V nB, double dA, double dB, V o, V d, double& t, int& st) {
+  double pr = dot(nA, d);
+  if (!(fabs(pr) > 0)) return false;
+  V N;
+  double D;
+  if (pr > 0) {
+    pr = dot(nB, d);
+    if (!(fabs(pr) > 0) || pr > 0) return false;
+    N = nB; D = dB; st = 1;
+  } else {
+    N = nA; D = dA; st = 0;
+  }
+  t = -(dot(N, o) + D) / pr;
+  if (!(t > EPS)) return false;
+  if (PLANE) return true;
+  V p = mk(d.x * t + o.x, d.y * t + o.y, d.z * t + o.z);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {  // checkInside (myPlanarObject.java:165-175, 200-211)
+    int vi = st ? (NV - 1 - i) : i;
+    int pi = st ? (NV - 1 - (i == 0 ? NV - 1 : i - 1)) : (i == 0 ? NV - 1 : i - 1);
+    V w = ld3(v[vi]), wp = ld3(v[pi]);
+    V e = sub(w, wp);
+    V ir = mk(p.x - w.x, p.y - w.y, p.z - w.z);
+    if (dot(cross(ir, e), N) < -EPS) return false;
+  }
+  return true;
+}
+
+DEVI bool tri_test(const TriD& T, V o, V d, double& t, int& st) {
+  V nA = ld3(T.n);
+  V nB = mk(-nA.x, -nA.y, -nA.z);  // exactly the reversed-order normal
+  return planar_test<3, false>(T.v, nA, nB, T.dA, T.dB, o, d, t, st);
+}
+
+DEVI V sphere_center(const PrimD& P, const Key& k, uint32_t site) {
+  if (P.type != PT_MSPHERE) return ld3(P.a);
+  // myMovingSphere.getOrigin(ray.getTime()) : keyed per (ray, object)
+  double tm = rng(k.seed, k.pixel, k.sample, k.node, site, P.key, 0, 1.0);
+  V o0 = ld3(P.a), o1 = ld3(P.a + 6);
+  V bMa = sub(o1, o0);
+  return mk(o0.x + tm * bMa.x, o0.y + tm * bMa.y, o0.z + tm * bMa.z);
+}
+
+DEVI bool prim_test(const PrimD& P, V o, V d, const Key& k, uint32_t tsite, double& t, int& args) {
+  switch (P.type) {
+    case PT_QUAD:
+    case PT_PLANE: {
+      const double(*v)[3] = (const double(*)[3])P.a;
+      if (P.type == PT_PLANE)
+        return planar_test<4, true>(v, ld3(P.a + 12), ld3(P.a + 15), P.a[18], P.a[19], o, d, t, args);
+      return planar_test<4, false>(v, ld3(P.a + 12), ld3(P.a + 15), P.a[18], P.a[19], o, d, t, args);
+    }
+    case PT_SPHERE:
+    case PT_MSPHERE: {  // mySphere.intersectCheck (myImpObject.java:76-94)
+      V c = sphere_center(P, k, tsite);
+      double rx = P.a[3], ry = P.a[4], rz = P.a[5];
+      double a = ((d.x / rx) * (d.x / rx)) + ((d.y / ry) * (d.y / ry)) + ((d.z / rz) * (d.z / rz));
+      V pC = mk((o.x - c.x) / rx, (o.y - c.y) / ry, (o.z - c.z) / rz);
+      double ta = 2 * a;
+      double b = 2 * (((d.x / rx) * pC.x) + ((d.y / ry) * pC.y) + ((d.z / rz) * pC.z));
+      double cc = (pC.x * pC.x) + (pC.y * pC.y) + (pC.z * pC.z) - 1;
+      double discr = ((b * b) - (2 * ta * cc));
+      if (discr < 0) return false;
+      double d1 = sqrt(discr), t1 = (-1 * b + d1) / (ta), t2 = (-1 * b - d1) / (ta);
+      double tv = jmin(t1, t2);
+      if (tv < EPS) {
+        tv = jmax(t1, t2);
+        if (tv < EPS) return false;
+      }
+      if (tv != tv) return false;  // reference: NaN t is never a closest hit (TreeMap orders NaN last)
+      t = tv;
+      args = 0;
+      return true;
+    }
+    case PT_CYL:
+    case PT_HCYL: {
+      double rx = P.a[3], rz = P.a[4], yTop = P.a[6], yBot = P.a[7];
+      V org = ld3(P.a);
+      double a = ((d.x / rx) * (d.x / rx)) + ((d.z / rz) * (d.z / rz));
+      double px = (o.x - org.x) / rx, pz = (o.z - org.z) / rz;
+      double b = 2 * (((d.x / rx) * px) + ((d.z / rz) * pz));
+      double cc = (px * px) + (pz * pz) - 1;
+      double discr = ((b * b) - (4 * a * cc));
+      if (discr < 0) return false;
+      double d1 = sqrt(discr), t1 = (-b + d1) / (2 * a), t2 = (-b - d1) / (2 * a);
+      double cv = jmin(t1, t2), co = jmax(t1, t2);
+      if (P.type == PT_HCYL) {  // myHollow_Cylinder.intersectCheck :174-192
+        if (cv < -EPS) {
+          double tmp = co; co = cv; cv = tmp;
+          if (cv < -EPS) return false;
+        }
+        double y1 = o.y + (cv * d.y);
+        if ((cv > EPS) && (y1 > yBot) && (y1 < yTop)) { t = cv; args = 0; return true; }
+        double y2 = o.y + (co * d.y);
+        if ((co > EPS) && (y2 > yBot) && (y2 < yTop)) { t = co; args = 1; return true; }
+        return false;
+      }
+      // myCylinder.intersectCheck :259-302
+      if (cv < EPS) {
+        co = cv;
+        cv = jmax(t1, t2);
+        if (cv < EPS) return false;
+      }
+      bool planeRes = true;
+      double pl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const double* cap = P.a + 8 + 4 * i;
+        double den = cap[0] * d.x + cap[1] * d.y + cap[2] * d.z;
+        if (fabs(den) > EPS) {
+          double nm = cap[0] * o.x + cap[1] * o.y + cap[2] * o.z + cap[3];
+          pl[i] = -nm / den;
+        } else {
+          pl[i] = 10000;
+        }
+      }
+      double pltVal = jmin(pl[0], pl[1]);
+      int idxVis = (pltVal == pl[0] ? 0 : 1);
+      if (pltVal < 0) {
+        pltVal = pl[idxVis];
+        if (pltVal < EPS) planeRes = false;
+      }
+      double tVal, maxT = jmax(cv, co), minT = jmin(cv, co);
+      if (planeRes && (((minT <= 0) && (pltVal >= -EPS) && (pltVal <= maxT)) || ((pltVal > minT) && (pltVal <= maxT)))) {
+        tVal = pltVal;
+      } else {
+        tVal = cv;
+        idxVis = 2;
+      }
+      double y1 = o.y + (tVal * d.y);
+      if ((y1 + EPS >= yBot) && (y1 - EPS <= yTop)) { t = tVal; args = idxVis; return true; }
+      return false;
+    }
+    case PT_BOX: {  // myRndrdBox -> myBBox.intersectCheck
+      double te;
+      if (!slab(P.a, P.a + 3, o, d, te)) return false;
+      t = te;
+      args = slab_plane(P.a, P.a + 3, o, d);
+      return true;
+    }
+  }
+  return false;
+}
+
+}  // namespace dv
+}  // namespace rt

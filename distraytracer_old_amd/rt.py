@@ -1,0 +1,193 @@
+"""ctypes binding of libdistraytracer.so (include/distraytracer.h).
+
+This is the product path: every render goes through the HIP kernels. There is
+no CPU fallback -- if the library is missing or no GPU is visible the calls
+raise RTError.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+import numpy as np
+
+from . import build as _build
+from .scenes import SCENE_DIR, prepare
+
+ST_NAMES = ["camera", "shadow", "refl", "refr", "box", "tri", "quad", "implicit", "light", "photon", "texel",
+            "node", "leaf", "member", "root"]
+INFO_NAMES = ["objects", "lights", "bvh_internal", "bvh_leaves", "bvh_depth", "bvh_prims", "prims",
+              "rays_per_pixel", "device_bytes", "triangles", "photons", "materials"]
+
+
+class RTError(RuntimeError):
+    pass
+
+
+class TextureDesc(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_int32), ("h", ctypes.c_int32), ("rgb", ctypes.c_void_p)]
+
+
+class RenderParams(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
+                ("row0", ctypes.c_int32), ("row1", ctypes.c_int32), ("row_step", ctypes.c_int32),
+                ("seed", ctypes.c_uint64), ("flags", ctypes.c_uint32), ("pad", ctypes.c_int32)]
+
+
+EXPORTS = ["rt_abi_version", "rt_last_error", "rt_device_count", "rt_scene_create", "rt_scene_load_cli",
+           "rt_scene_inspect_cli",
+           "rt_scene_info", "rt_scene_destroy", "rt_photons_build", "rt_render", "rt_render_device",
+           "rt_render_count", "rt_time_render"]
+
+_lib = None
+
+
+def lib_path() -> Path:
+    return _build.LIB_PATH
+
+
+def lib():
+    """Load the HIP library; raises RTError (never falls back) if it is absent."""
+    global _lib
+    if _lib is None:
+        p = lib_path()
+        if not p.exists():
+            raise RTError(f"{p} is missing: build it with `python -m distraytracer_old_amd.build`")
+        L = ctypes.CDLL(str(p))
+        L.rt_last_error.restype = ctypes.c_char_p
+        L.rt_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.rt_scene_load_cli.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(TextureDesc),
+                                        ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.rt_scene_inspect_cli.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(TextureDesc),
+                                           ctypes.c_void_p, ctypes.c_int]
+        L.rt_scene_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.rt_scene_destroy.argtypes = [ctypes.c_void_p]
+        L.rt_photons_build.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.rt_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_void_p]
+        L.rt_render_count.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p]
+        L.rt_render_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p]
+        L.rt_time_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_double)]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise RTError(f"{what} failed ({rc}): {lib().rt_last_error().decode()}")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _check(lib().rt_device_count(ctypes.byref(n)), "rt_device_count")
+    return n.value
+
+
+def _tex_args(textures: dict):
+    names = list(textures)
+    arrs = [np.ascontiguousarray(textures[n], dtype=np.uint8) for n in names]
+    cnames = (ctypes.c_char_p * max(1, len(names)))(*[n.encode() for n in names])
+    tds = (TextureDesc * max(1, len(names)))(*[TextureDesc(a.shape[1], a.shape[0], a.ctypes.data) for a in arrs])
+    return names, arrs, cnames, tds
+
+
+def inspect_cli(cli: str, scene_dir=SCENE_DIR, textures: dict | None = None) -> dict:
+    """Host-only parse + flatten + BVH build (no GPU needed)."""
+    if textures is None:
+        textures = prepare(cli, Path(scene_dir))
+    names, arrs, cnames, tds = _tex_args(textures)
+    v = np.zeros(12, dtype=np.int64)
+    _check(lib().rt_scene_inspect_cli(str(scene_dir).encode(), cli.encode(), len(names), cnames, tds,
+                                      v.ctypes.data, 12), "rt_scene_inspect_cli")
+    return dict(zip(INFO_NAMES, v.tolist()))
+
+
+def params(W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1) -> RenderParams:
+    r0, r1 = (0, H) if rows is None else rows
+    return RenderParams(W, H, spp, r0, r1, row_step, seed, 0, 0)
+
+
+def nrows_of(p: RenderParams) -> int:
+    r1 = p.row1 if p.row1 > 0 else p.height
+    step = max(1, p.row_step)
+    return (r1 - p.row0 + step - 1) // step
+
+
+class Scene:
+    """A scene resident on one GPU (rt_scene*)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def load_cli(cls, cli: str, scene_dir=SCENE_DIR, textures: dict | None = None, device: int = 0) -> "Scene":
+        if textures is None:
+            textures = prepare(cli, Path(scene_dir))
+        names, arrs, cnames, tds = _tex_args(textures)
+        h = ctypes.c_void_p()
+        _check(lib().rt_scene_load_cli(str(scene_dir).encode(), cli.encode(), len(names), cnames, tds, device,
+                                       ctypes.byref(h)), "rt_scene_load_cli")
+        return cls(h)
+
+    def info(self) -> dict:
+        v = np.zeros(12, dtype=np.int64)
+        _check(lib().rt_scene_info(self._h, v.ctypes.data, 12), "rt_scene_info")
+        return dict(zip(INFO_NAMES, v.tolist()))
+
+    def build_photons(self, seed: int):
+        _check(lib().rt_photons_build(self._h, seed), "rt_photons_build")
+
+    def render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1):
+        p = params(W, H, spp, seed, rows, row_step)
+        n = nrows_of(p)
+        rgb = np.zeros((n, W, 3), dtype=np.float32)
+        argb = np.zeros((n, W), dtype=np.int32)
+        _check(lib().rt_render(self._h, ctypes.byref(p), rgb.ctypes.data, argb.ctypes.data), "rt_render")
+        return rgb, argb
+
+    def render_count(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1):
+        p = params(W, H, spp, seed, rows, row_step)
+        n = nrows_of(p)
+        rgb = np.zeros((n, W, 3), dtype=np.float32)
+        argb = np.zeros((n, W), dtype=np.int32)
+        st = np.zeros(16, dtype=np.uint64)
+        _check(lib().rt_render_count(self._h, ctypes.byref(p), rgb.ctypes.data, argb.ctypes.data, st.ctypes.data),
+               "rt_render_count")
+        return rgb, argb, dict(zip(ST_NAMES, st[: len(ST_NAMES)].tolist()))
+
+    def render_device(self, p: RenderParams, rgb_ptr: int, argb_ptr: int, stream: int = 0):
+        """Asynchronous render into device buffers (e.g. torch tensors' data_ptr()) on a HIP stream."""
+        _check(lib().rt_render_device(self._h, ctypes.byref(p), ctypes.c_void_p(rgb_ptr), ctypes.c_void_p(argb_ptr),
+                                      ctypes.c_void_p(stream)), "rt_render_device")
+
+    def time_render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, warmup=1, iters=3) -> float:
+        p = params(W, H, spp, seed, rows, row_step)
+        ms = ctypes.c_double(0)
+        _check(lib().rt_time_render(self._h, ctypes.byref(p), warmup, iters, ctypes.byref(ms)), "rt_time_render")
+        return ms.value
+
+    def close(self):
+        if self._h:
+            lib().rt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def argb_to_rgb8(argb: np.ndarray) -> np.ndarray:
+    a = argb.view(np.uint32)
+    return np.stack([(a >> 16) & 255, (a >> 8) & 255, a & 255], -1).astype(np.uint8)

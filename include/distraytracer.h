@@ -1,0 +1,185 @@
+/*
+ * distraytracer.h -- C ABI of the MI355X-native trace loop (libdistraytracer.so).
+ *
+ * Drop-in boundary for the reference's render entry, the abstract
+ * `myScene.draw()` (src/rayTracerDistAccelShdPhtnMap/myScene.java:1182),
+ * implemented by `myFOVScene.draw()` (myScene.java:1481-1531) and reached from
+ * the `.cli` `write` command (myRTFileReader.java:86-93) and from
+ * `DistRayTracer.draw()` (DistRayTracer.java:77). Everything below that call
+ * -- shootMultiRays (:1447), reflectRay (:907), findClosestRayHit (:888),
+ * calcShadow (:879), the myGeomBase/myBVH traversal (myGeomBase.java:132-421),
+ * myObjShader.getColorAtPos (myObjShader.java:409) and the photon kNN gather
+ * (myLight.java:389-445) -- runs as HIP kernels on gfx950.
+ *
+ * Two ways in:
+ *   rt_scene_create(desc)  the flattened myScene the Java side would hand over
+ *                          through JNI (objList/lightList/shaders/CTMs/accel
+ *                          groups; INTEGRATION.md shows the binding);
+ *   rt_scene_load_cli()    the native mirror of myRTFileReader.readRTFile
+ *                          (myRTFileReader.java:15-349) that builds that same
+ *                          desc from a `.cli` file, then calls rt_scene_create.
+ *
+ * Conventions: every function returns 0 on success or a negative RT_E* code;
+ * rt_last_error() gives a thread-local message. No exceptions or longjmp cross
+ * the ABI. Output buffers are caller-owned and never retained. One in-flight
+ * render per scene; distinct scenes may render concurrently. Products of this
+ * library are GPU-only: there is no CPU fallback (RT_E_NODEVICE when no GPU).
+ */
+#ifndef DISTRAYTRACER_H
+#define DISTRAYTRACER_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum rt_status {
+  RT_OK = 0,
+  RT_E_INVALID = -1,  /* bad argument / malformed desc */
+  RT_E_PARSE = -2,    /* .cli parse error or unsupported command */
+  RT_E_IO = -3,       /* file not found */
+  RT_E_NODEVICE = -4, /* no HIP device */
+  RT_E_HIP = -5,      /* HIP runtime error */
+  RT_E_OOM = -6
+};
+
+/* primitive kinds (objType.java; readPrimData myScene.java:447-521) */
+enum rt_prim_type {
+  RT_PRIM_TRIANGLE = 0,  /* myTriangle */
+  RT_PRIM_QUAD = 1,      /* myQuad */
+  RT_PRIM_PLANE = 2,     /* myPlane (infinite) */
+  RT_PRIM_SPHERE = 3,    /* mySphere / ellipsoid / sphereIn */
+  RT_PRIM_MOVING_SPHERE = 4,
+  RT_PRIM_CYLINDER = 5,  /* myCylinder (capped) */
+  RT_PRIM_HOLLOW_CYLINDER = 6,
+  RT_PRIM_BOX = 7        /* myRndrdBox */
+};
+#define RT_PRIM_INVERTED 1 /* sphereIn: normals point in (mySceneObject.invertedIDX) */
+
+typedef struct rt_prim_desc {
+  int32_t type;     /* rt_prim_type */
+  int32_t material; /* index into rt_scene_desc.materials */
+  int32_t flags;    /* RT_PRIM_INVERTED */
+  int32_t nverts;   /* planar: 3 or 4 */
+  double ctm[16];   /* row-major CTM: matrix-stack top when the object was created */
+  double v[4][3];   /* planar vertices in file order */
+  double uv[4][2];  /* texture_coord per vertex */
+  /* sphere: cx cy cz rx ry rz [x1 y1 z1 for moving]; cylinder: r h cx cy cz ox oy oz;
+     box: xmin ymin zmin xmax ymax zmax; plane: a b c d */
+  double p[12];
+} rt_prim_desc;
+
+enum rt_texture_kind { RT_TEX_NONE = 0, RT_TEX_IMAGE = 1, RT_TEX_NOISE = 2, RT_TEX_MARBLE = 4 };
+
+typedef struct rt_material_desc { /* myObjShader.setCurrColors (myObjShader.java:51-75) */
+  int32_t simple;       /* 1 = mySimpleReflObjShdr (`shiny` with ktrans/index) */
+  int32_t texture;      /* rt_texture_kind */
+  int32_t tex_top;      /* texture index for RT_TEX_IMAGE "top", -1 none */
+  int32_t use_photon_map, caustic_photons;
+  int32_t octaves, rnd_colors, use_fwd_trans;
+  double diffuse[3], ambient[3], specular[3]; /* already clamped <= 1 (myColor) */
+  double phong_exp, k_refl, k_refl_clr[3], k_trans, perm, perm_clr[3];
+  double noise_scale, turb_mult, color_scale, color_mult, period_mult[3];
+  double colors[2][3];
+} rt_material_desc;
+
+enum rt_light_type { RT_LIGHT_POINT = 0, RT_LIGHT_SPOT = 1, RT_LIGHT_DISK = 2 };
+typedef struct rt_light_desc { /* myLight.java */
+  int32_t type, pad;
+  double pos[3], color[3], dir[3];
+  double inner_deg, outer_deg, radius;
+  double ctm[16];
+} rt_light_desc;
+
+typedef struct rt_accel_desc { /* myScene.endTmpObjList (myScene.java:305-324) */
+  int32_t type;        /* 0 = end_list (myGeomList), 1 = end_accel (myBVH) */
+  int32_t first, count; /* range of rt_scene_desc.accel_members (prim indices, tmp-list order) */
+  int32_t pad;
+  double ctm[16];      /* CTM when end_list/end_accel ran */
+} rt_accel_desc;
+
+typedef struct rt_texture_desc {
+  int32_t w, h;
+  const uint8_t* rgb; /* w*h*3 RGB8, row-major, row 0 = top (Processing PImage order) */
+} rt_texture_desc;
+
+typedef struct rt_scene_desc {
+  int32_t num_prims;
+  const rt_prim_desc* prims; /* every renderable primitive, creation order (= RNG prim key) */
+  int32_t num_materials;
+  const rt_material_desc* materials;
+  int32_t num_lights;
+  const rt_light_desc* lights; /* lightList order */
+  int32_t num_accels;
+  const rt_accel_desc* accels;
+  const int32_t* accel_members;
+  int32_t num_top;
+  const int32_t* top; /* objList order: >= 0 prim index, < 0 accel ~index */
+  int32_t num_textures;
+  const rt_texture_desc* textures;
+  double fov;            /* degrees */
+  double background[3];
+  int32_t bkg_texture;   /* -1 none; else skydome texture index */
+  int32_t rays_per_pixel;
+  double skydome[4];     /* radius, cx, cy, cz */
+  int32_t dof, pad0;
+  double lens_radius, lens_focal;
+  int32_t photon_mode;   /* 0 none, 1 diffuse_photons, 2 caustic_photons */
+  int32_t photon_count, photon_k, pad1;
+  double photon_max_dist; /* already rounded through float (Float.parseFloat) */
+} rt_scene_desc;
+
+typedef struct rt_render_params {
+  int32_t width, height; /* image size (the reference hard-codes 300x300, DistRayTracer.java:15-16) */
+  int32_t spp;           /* <= 0: the scene's rays_per_pixel */
+  int32_t row0, row1;    /* rows [row0,row1) of the image; row1 <= 0 means height */
+  int32_t row_step;      /* <= 1: every row; >1: interleaved rows (multi-GPU bands) */
+  uint64_t seed;         /* keyed RNG seed */
+  uint32_t flags;        /* reserved, 0 */
+  int32_t pad;
+} rt_render_params;
+
+typedef struct rt_scene rt_scene;
+
+/* counters (RT_ST_*) reported by rt_render_count */
+enum {
+  RT_ST_CAMERA = 0, RT_ST_SHADOW, RT_ST_REFL, RT_ST_REFR, RT_ST_BOX, RT_ST_TRI, RT_ST_QUAD, RT_ST_IMPLICIT,
+  RT_ST_LIGHT, RT_ST_PHOTON, RT_ST_TEXEL, RT_ST_NODE, RT_ST_N = 16
+};
+
+int rt_abi_version(void);
+const char* rt_last_error(void);
+int rt_device_count(int* count);
+
+int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out);
+int rt_scene_load_cli(const char* scene_dir, const char* cli_file, int num_textures, const char* const* texture_names,
+                      const rt_texture_desc* textures, int device, rt_scene** out);
+/* Host-only parse + build (no device): fills the rt_scene_info fields; device bytes = layout bytes. */
+int rt_scene_inspect_cli(const char* scene_dir, const char* cli_file, int num_textures, const char* const* texture_names,
+                         const rt_texture_desc* textures, int64_t* info, int n);
+/* info[0..11]: objects, lights, bvh_internal, bvh_leaves, bvh_depth, bvh_prims, prims, rays_per_pixel,
+   device bytes, triangles, photons, materials */
+int rt_scene_info(const rt_scene* scene, int64_t* info, int n);
+void rt_scene_destroy(rt_scene* scene);
+
+/* photon-map pre-pass (myScene.initRender :1096-1099); idempotent per scene */
+int rt_photons_build(rt_scene* scene, uint64_t seed);
+
+/* Blocking render into caller-owned HOST buffers (either may be NULL).
+   rgb: float[n_rows*width*3] clamped <=1 per myColor; argb: int32[n_rows*width], reference packing. */
+int rt_render(rt_scene* scene, const rt_render_params* p, float* rgb, int32_t* argb);
+/* Asynchronous render into caller-owned DEVICE buffers on `hip_stream` (hipStream_t, may be NULL). */
+int rt_render_device(rt_scene* scene, const rt_render_params* p, float* d_rgb, int32_t* d_argb, void* hip_stream);
+/* Instrumented render (per-lane counters, RT_ST_*): same image, slower; stats: uint64[RT_ST_N]. */
+int rt_render_count(rt_scene* scene, const rt_render_params* p, float* rgb, int32_t* argb, uint64_t* stats);
+/* Kernel-only timing helper: average ms of the render kernel over `iters` launches (HIP events on the
+   launch stream), inputs resident in HBM. */
+int rt_time_render(rt_scene* scene, const rt_render_params* p, int warmup, int iters, double* avg_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DISTRAYTRACER_H */

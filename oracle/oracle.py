@@ -81,7 +81,7 @@ class OracleScene:
         rgb = np.zeros((n, W, 3), dtype=np.float32)
         argb = np.zeros((n, W), dtype=np.int32)
         st = np.zeros(16, dtype=np.uint64)
-        nt = threads if threads > 0 else (os.cpu_count() or 1)
+        nt = threads if threads > 0 else min(16, os.cpu_count() or 1)  # GPU box CPU share is 16
         rc = lib().oracle_render(self._h, W, H, spp, seed, r0, r1, row_step, rgb.ctypes.data, argb.ctypes.data,
                                  st.ctypes.data, nt)
         if rc != 0:
