@@ -340,6 +340,7 @@ struct Builder {
     }
     for (int a = 0; a < d->num_accels; ++a)
       if (!build_accel(a)) return false;
+    if (hs.bvhDepth > 40) { err = "BVH deeper than the kernel traversal stack (40)"; return false; }
     for (int k = 0; k < d->num_top; ++k) {
       int32_t t = d->top[k];
       TopD td;
