@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Benchmark: the reference's headline workload on MI355X (BASELINE.json).
+
+metric  "Mray/s + achieved HBM GB/s, bun69k.cli 1024^2 16spp, 1/2/4/8 GPU"
+workload C3 = scenes/c3_bun69k.cli (data/p3_t09.cli without `wood`) with the
+         synthetic bun69k (69,451 triangles), 1024x1024, 16 spp, seed 0x5EED0001.
+
+One step = one full C3 frame: every rank renders its rows (rank r renders rows
+r, r+N, r+2N, ... -- interleaved for load balance) with the HIP kernel into a
+device buffer, then (N>1) the per-rank float-RGB tiles are gathered to rank 0
+over RCCL (`all_gather_into_tensor`). Work per step is one frame whatever N is
+(strong scaling). value = traced rays of the frame (camera + shadow + reflection
++ refraction, counted exactly by an instrumented run before timing) / max-over-
+ranks step time.
+
+roofline: algorithmic bytes of the render kernel per launch (record sizes x the
+instrumented counters, DESIGN.md "Algorithmic bytes") / its mean duration from
+HIP events on the launch stream; peak 8000 GB/s (MI355X HBM3E). traffic: HBM
+bytes from a committed rocprofv3 --pmc FETCH_SIZE run (x2, gfx950 half-count) if
+present in profiles/, else null.
+
+cpu_baseline: the oracle (CPU restatement of the reference path, fp64) timed on
+host cores on a row subsample of the same frame (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+METRIC = "Mray/s + achieved HBM GB/s, bun69k.cli 1024² 16spp, 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# record bytes per counted event (rt_types.h layouts; DESIGN.md "Algorithmic bytes")
+RECORD_BYTES = {
+    "node": 128,      # NodeD: both child boxes of an internal node
+    "tri": 128,       # TriD
+    "quad": 256,      # PrimD (planar)
+    "implicit": 256,  # PrimD (sphere / cylinder / box)
+    "leaf": 8,        # LeafD
+    "member": 4,      # leaf member ref
+    "root": 64,       # AccelD root box
+    "top": 16 + 96,   # TopD + the 3 used rows of the inverse CTM
+    "light": 272,     # LightD
+    "photon": 64,     # PhotonD
+    "texel": 16,      # 4 texels of a bilinear lookup
+}
+
+
+def algorithmic_bytes(st: dict) -> int:
+    return int(sum(st.get(k, 0) * b for k, b in RECORD_BYTES.items()))
+
+
+def traced_rays(st: dict) -> int:
+    return int(st["camera"] + st["shadow"] + st["refl"] + st["refr"])
+
+
+def find_traffic(workload: str):
+    """Per-launch HBM bytes from the newest committed PMC summary for this workload."""
+    files = sorted(glob.glob(str(REPO / "profiles" / "*pmc*.json")))
+    for f in reversed(files):
+        try:
+            d = json.loads(Path(f).read_text())
+        except Exception:
+            continue
+        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+            return float(d["hbm_bytes_per_launch"]), Path(f).name
+    return None, None
+
+
+def cpu_baseline(cli, W, H, spp, seed, tex, row_step=4, threads=16):
+    from oracle.oracle import OracleScene
+
+    threads = min(threads, os.cpu_count() or 1)
+    o = OracleScene(REPO / "scenes", cli, tex)
+    o.render(W, H, spp=spp, seed=seed, rows=(0, H), row_step=512, threads=threads)  # warm caches
+    t0 = time.perf_counter()
+    _, _, st = o.render(W, H, spp=spp, seed=seed, rows=(0, H), row_step=row_step, threads=threads)
+    dt = time.perf_counter() - t0
+    rays = traced_rays(st)
+    # single-thread rate (mirrors the single-threaded Java reference) on a smaller sample
+    t1 = time.perf_counter()
+    _, _, st1 = o.render(W, H, spp=spp, seed=seed, rows=(1, H), row_step=64, threads=1)
+    dt1 = time.perf_counter() - t1
+    o.close()
+    return {
+        "value": rays / dt / 1e6,
+        "unit": "Mray/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"oracle (fp64 C++ restatement) on rows 0::{row_step} of the {W}x{H}x{spp} frame "
+                  f"({rays} rays, {dt:.2f} s on {threads} threads)",
+        "value_1thread": traced_rays(st1) / dt1 / 1e6,
+        "sample_1thread": f"rows 1::64 ({traced_rays(st1)} rays, {dt1:.2f} s, 1 thread)",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    from distraytracer_old_amd import rt, scenes
+
+    cli, W, H, spp, seed = scenes.CONFIGS[args.config]
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    tex = scenes.prepare(cli)
+    scene = rt.Scene.load_cli(cli, textures=tex, device=local)
+    # this rank's rows: r, r+N, ...
+    p = rt.params(W, H, spp=spp, seed=seed, rows=(rank, H), row_step=world)
+    nrows = rt.nrows_of(p)
+    maxrows = (H + world - 1) // world
+
+    # exact per-frame counters (instrumented run, outside the timed region)
+    _, _, st = scene.render_count(W, H, spp=spp, seed=seed, rows=(rank, H), row_step=world)
+    counts = torch.tensor([traced_rays(st), algorithmic_bytes(st), st["camera"]], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(counts)
+    rays_frame, bytes_frame, cam_frame = [float(x) for x in counts.tolist()]
+    my_bytes = float(algorithmic_bytes(st))
+
+    rgb = torch.empty((maxrows, W, 3), dtype=torch.float32, device="cuda")
+    argb = torch.empty((maxrows, W), dtype=torch.int32, device="cuda")
+    gathered = torch.empty((world, maxrows, W, 3), dtype=torch.float32, device="cuda") if dist else None
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        scene.render_device(p, rgb.data_ptr(), argb.data_ptr(), stream.cuda_stream)
+        if ev:
+            ev[1].record(stream)
+        if dist:
+            dist.all_gather_into_tensor(gathered.view(-1), rgb.view(-1))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    t = torch.tensor([dt, kern_ms], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt, kern_ms_max = t.tolist()
+    ms_per_step = dt / args.steps * 1e3
+
+    if rank == 0:
+        # rank-0 kernel: its own algorithmic bytes over its own mean kernel duration
+        achieved = my_bytes / (kern_ms / 1e3) / 1e9
+        workload = f"{args.config} {cli} {W}x{H} {spp}spp"
+        traffic, tsrc = find_traffic(workload)
+        out = {
+            "metric": METRIC,
+            "value": rays_frame / (ms_per_step / 1e3) / 1e6,
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: bun69k = deterministic subdivision of data/bun500.cli (69,451 tris); "
+                    "scene data/p3_t09.cli without the wood line",
+            "config": {"workload": workload, "width": W, "height": H, "spp": spp, "seed": seed,
+                       "rays_per_frame": int(rays_frame), "camera_samples": int(cam_frame),
+                       "parallelism": f"rows interleaved over {world} rank(s)" +
+                                      (" + RCCL all_gather of float RGB tiles" if world > 1 else "")},
+            "camera_msamples_per_s": cam_frame / (ms_per_step / 1e3) / 1e6,
+            "achieved_hbm_gbps": achieved,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS,
+                         "traffic": traffic, "traffic_source": tsrc,
+                         "kernel": "render_kernel", "kernel_ms": kern_ms,
+                         "bytes_per_launch": my_bytes, "bytes_per_ray": bytes_frame / max(1.0, rays_frame)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cli, W, H, spp, seed, tex)
+        print(json.dumps(out), flush=True)
+    scene.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

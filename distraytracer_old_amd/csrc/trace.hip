@@ -130,6 +130,7 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
   Best best = miss();
   for (int i = 0; i < S.ntop; ++i) {
     TopD tp = S.top[i];
+    if (CNT) ct.c[C_TOP]++;
     renorm(w);
     const double* inv = S.xf[tp.xf].inv;
     V o = xpt(inv, w.o), d = xvec(inv, w.d);
@@ -221,6 +222,7 @@ template <bool CNT>
 DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, uint32_t tsite, double dist, Counters& ct) {
   for (int i = 0; i < S.ntop; ++i) {
     TopD tp = S.top[i];
+    if (CNT) ct.c[C_TOP]++;
     renorm(w);
     const double* inv = S.xf[tp.xf].inv;
     V o = xpt(inv, w.o), d = xvec(inv, w.d);

@@ -27,7 +27,7 @@ enum : uint32_t {
   SITE_DISK = 0x100, SITE_SHADOW_TIME = 0x200
 };
 enum { C_CAMERA = 0, C_SHADOW, C_REFL, C_REFR, C_BOX, C_TRI, C_QUAD, C_IMPLICIT, C_LIGHT, C_PHOTON, C_TEXEL,
-       C_NODE, C_LEAF, C_MEMBER, C_ROOT, C_N = 16 };
+       C_NODE, C_LEAF, C_MEMBER, C_ROOT, C_TOP, C_N = 16 };
 
 struct V {
   double x, y, z;

@@ -15,7 +15,7 @@ from . import build as _build
 from .scenes import SCENE_DIR, prepare
 
 ST_NAMES = ["camera", "shadow", "refl", "refr", "box", "tri", "quad", "implicit", "light", "photon", "texel",
-            "node", "leaf", "member", "root"]
+            "node", "leaf", "member", "root", "top"]
 INFO_NAMES = ["objects", "lights", "bvh_internal", "bvh_leaves", "bvh_depth", "bvh_prims", "prims",
               "rays_per_pixel", "device_bytes", "triangles", "photons", "materials"]
 

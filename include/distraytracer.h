@@ -147,7 +147,8 @@ typedef struct rt_scene rt_scene;
 /* counters (RT_ST_*) reported by rt_render_count */
 enum {
   RT_ST_CAMERA = 0, RT_ST_SHADOW, RT_ST_REFL, RT_ST_REFR, RT_ST_BOX, RT_ST_TRI, RT_ST_QUAD, RT_ST_IMPLICIT,
-  RT_ST_LIGHT, RT_ST_PHOTON, RT_ST_TEXEL, RT_ST_NODE, RT_ST_N = 16
+  RT_ST_LIGHT, RT_ST_PHOTON, RT_ST_TEXEL, RT_ST_NODE, RT_ST_LEAF, RT_ST_MEMBER, RT_ST_ROOT, RT_ST_TOP,
+  RT_ST_N = 16
 };
 
 int rt_abi_version(void);

@@ -1,0 +1,34 @@
+"""Summarise rocprofv3 CSV output (kernel stats and FETCH_SIZE PMC) into profiles/.
+
+usage: python tools/pmc_summary.py <kernel_stats.csv> <counter_collection.csv|-> <workload> <out.json>
+FETCH_SIZE is reported in KB; on gfx950 it counts half the bytes of wide
+coalesced reads (MI355X_MICROARCH.md "HBM"), so hbm = FETCH_SIZE * 1024 * 2.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+stats_csv, pmc_csv, workload, out = sys.argv[1:5]
+res = {"workload": workload, "kernels": {}}
+with open(stats_csv) as f:
+    for r in csv.DictReader(f):
+        name = r.get("Name") or r.get("KernelName") or ""
+        res["kernels"][name] = {k: r[k] for k in r if k != "Name"}
+if pmc_csv != "-":
+    per = defaultdict(list)
+    with open(pmc_csv) as f:
+        for r in csv.DictReader(f):
+            if r.get("Counter_Name") != "FETCH_SIZE":
+                continue
+            name = r.get("Kernel_Name", "")
+            per[name].append(float(r["Counter_Value"]))
+    res["fetch_size_kb"] = {k: v for k, v in per.items()}
+    kern = [k for k in per if "render_kernel" in k and "ILb0" in k]
+    if kern:
+        vals = per[kern[0]]
+        kb = sum(vals) / len(vals)
+        res["hbm_bytes_per_launch"] = kb * 1024 * 2
+        res["hbm_kernel"] = kern[0]
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps({k: v for k, v in res.items() if k != "kernels"})[:2000])
