@@ -75,7 +75,7 @@ def find_traffic(workload: str):
     return None, None
 
 
-def cpu_baseline(cli, W, H, spp, seed, tex, row_step=4, threads=16):
+def cpu_baseline(cli, W, H, spp, seed, tex, row_step=1, threads=16):
     from oracle.oracle import OracleScene
 
     threads = min(threads, os.cpu_count() or 1)
@@ -87,7 +87,7 @@ def cpu_baseline(cli, W, H, spp, seed, tex, row_step=4, threads=16):
     rays = traced_rays(st)
     # single-thread rate (mirrors the single-threaded Java reference) on a smaller sample
     t1 = time.perf_counter()
-    _, _, st1 = o.render(W, H, spp=spp, seed=seed, rows=(1, H), row_step=64, threads=1)
+    _, _, st1 = o.render(W, H, spp=spp, seed=seed, rows=(1, H), row_step=16, threads=1)
     dt1 = time.perf_counter() - t1
     o.close()
     return {
@@ -98,7 +98,7 @@ def cpu_baseline(cli, W, H, spp, seed, tex, row_step=4, threads=16):
         "sample": f"oracle (fp64 C++ restatement) on rows 0::{row_step} of the {W}x{H}x{spp} frame "
                   f"({rays} rays, {dt:.2f} s on {threads} threads)",
         "value_1thread": traced_rays(st1) / dt1 / 1e6,
-        "sample_1thread": f"rows 1::64 ({traced_rays(st1)} rays, {dt1:.2f} s, 1 thread)",
+        "sample_1thread": f"rows 1::16 ({traced_rays(st1)} rays, {dt1:.2f} s, 1 thread)",
     }
 
 
@@ -146,7 +146,9 @@ def main():
     rgb = torch.empty((maxrows, W, 3), dtype=torch.float32, device="cuda")
     argb = torch.empty((maxrows, W), dtype=torch.int32, device="cuda")
     gathered = torch.empty((world, maxrows, W, 3), dtype=torch.float32, device="cuda") if dist else None
+    from distraytracer_old_amd import multigpu
     stream = torch.cuda.current_stream()
+    full_img = torch.empty((H, W, 3), dtype=torch.float32, device="cuda") if dist and rank == 0 else None
 
     def step(ev=None):
         if ev:
@@ -154,8 +156,10 @@ def main():
         scene.render_device(p, rgb.data_ptr(), argb.data_ptr(), stream.cuda_stream)
         if ev:
             ev[1].record(stream)
-        if dist:
+        if dist:  # the single exchange: float-RGB tiles over RCCL, re-interleaved on rank 0
             dist.all_gather_into_tensor(gathered.view(-1), rgb.view(-1))
+            if rank == 0:
+                full_img[:] = multigpu.assemble(gathered, H)
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,72 @@
+"""C-ABI boundary (include/distraytracer.h): library loads, exports every declared
+entry point, reports errors with the documented codes, and the host-side loader +
+BVH builder reproduce the oracle's scene topology. No GPU needed."""
+import re
+import tempfile
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from distraytracer_old_amd import rt, scenes
+from oracle.oracle import OracleScene
+
+HEADER = Path(__file__).resolve().parent.parent / "include" / "distraytracer.h"
+
+
+def declared():
+    txt = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = rt.lib()
+    names = declared()
+    assert len(names) >= 12
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(rt.EXPORTS)
+    assert L.rt_abi_version() == 1
+
+
+def test_no_gpu_fails_loudly():
+    if rt.device_count() > 0:
+        pytest.skip("GPU present")
+    with pytest.raises(rt.RTError, match="no HIP device"):
+        rt.Scene.load_cli("t01.cli")
+
+
+def test_error_codes():
+    L = rt.lib()
+    info = np.zeros(12, dtype=np.int64)
+    assert L.rt_scene_inspect_cli(str(scenes.SCENE_DIR).encode(), b"does_not_exist.cli", 0, None, None,
+                                  info.ctypes.data, 12) == -3  # RT_E_IO
+    d = Path(tempfile.mkdtemp())
+    (d / "bad.cli").write_text("fov 60\nnamed_object foo\n")
+    assert L.rt_scene_inspect_cli(str(d).encode(), b"bad.cli", 0, None, None, info.ctypes.data, 12) == -2
+    assert b"unsupported command" in L.rt_last_error()
+    (d / "bad2.cli").write_text("fov 60\nsphere 1 0 0\n")
+    assert L.rt_scene_inspect_cli(str(d).encode(), b"bad2.cli", 0, None, None, info.ctypes.data, 12) == -2
+    assert L.rt_scene_inspect_cli(None, b"x.cli", 0, None, None, info.ctypes.data, 12) == -1
+    with pytest.raises(rt.RTError):
+        rt.inspect_cli("plnts3ColsBunnies.cli", textures={})  # texture not registered
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4", "C5"])
+def test_host_builder_matches_oracle_topology(cfg):
+    cli = scenes.CONFIGS[cfg][0]
+    tex = scenes.prepare(cli)
+    a = rt.inspect_cli(cli, textures=tex)
+    b = OracleScene(scenes.SCENE_DIR, cli, tex).info()
+    for k, v in b.items():
+        assert a[k] == v, (cfg, k, a[k], v)
+
+
+@pytest.mark.parametrize("cli", ["p2_t03.cli", "p2_t05.cli", "p2_t07.cli", "c2clear.cli", "t05.cli", "p3_t05.cli",
+                                 "earth.cli", "cylinder1.cli"])
+def test_host_builder_feature_scenes(cli):
+    tex = scenes.prepare(cli)
+    a = rt.inspect_cli(cli, textures=tex)
+    b = OracleScene(scenes.SCENE_DIR, cli, tex).info()
+    for k, v in b.items():
+        assert a[k] == v, (cli, k, a[k], v)
