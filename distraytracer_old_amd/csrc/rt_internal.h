@@ -42,6 +42,8 @@ struct HostScene {
 };
 
 int build_host_scene(const rt_scene_desc* d, HostScene& hs);  // scene_build.cpp
+// photon.cpp: kd-tree over photons in insertion order (myKD_Tree.build_tree, myLight.java:325-381)
+void build_photon_tree(HostScene& hs, const std::vector<double>& pos, const std::vector<double>& pwr);
 
 }  // namespace rt
 

@@ -35,14 +35,14 @@ struct Best {
 DEVI Best miss() { Best b; b.t = DMAX; b.ref = 0; b.top = -1; b.inAcc = 0; b.dw = mk(0, 0, 0); return b; }
 
 template <bool CNT>
-DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, uint32_t tsite, double& t, int& args, Counters& ct) {
+DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, double& t, int& args, Counters& ct) {
   if (ref >= 0) {
     if (CNT) ct.c[C_TRI]++;
     return tri_test(S.tri[ref], o, d, t, args);
   }
   const PrimD& P = S.prim[~ref];
   if (CNT) { if (P.type == PT_QUAD || P.type == PT_PLANE) ct.c[C_QUAD]++; else ct.c[C_IMPLICIT]++; }
-  return prim_test(P, o, d, k, tsite, t, args);
+  return prim_test(P, o, d, k, t, args);
 }
 DEVI int32_t ref_xf(const SceneD& S, int32_t ref) { return ref >= 0 ? S.tri[ref].xf : S.prim[~ref].xf; }
 
@@ -60,7 +60,7 @@ DEVI void leaf_closest(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w
     else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
     double t;
     int args;
-    if (test_ref<CNT>(S, ref, o, d, k, SITE_TIME, t, args, ct) && t < cur.t) {
+    if (test_ref<CNT>(S, ref, o, d, k, t, args, ct) && t < cur.t) {
       cur.t = t; cur.ref = ref; cur.inAcc = 1; cur.dw = w.d;
     }
   }
@@ -147,7 +147,7 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
       int args;
-      if (test_ref<CNT>(S, ref, o, d, k, SITE_TIME, t, args, ct) && t < best.t) {
+      if (test_ref<CNT>(S, ref, o, d, k, t, args, ct) && t < best.t) {
         best.t = t; best.ref = ref; best.top = i; best.inAcc = 0; best.dw = w.d;
       }
     }
@@ -164,7 +164,7 @@ DEVI bool shadow_box(const double* mn, const double* mx, V o, V d, double dist, 
   return slab(mn, mx, o, d, te) && (dist - te) > EPS;
 }
 template <bool CNT>
-DEVI bool leaf_any(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, const Key& k, uint32_t tsite, double dist, Counters& ct) {
+DEVI bool leaf_any(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
   LeafD lf = S.leaf[leaf];
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
   for (int i = 0; i < lf.count; ++i) {
@@ -176,15 +176,15 @@ DEVI bool leaf_any(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, co
     else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
     double t;
     int args;
-    if (test_ref<CNT>(S, ref, o, d, k, tsite, t, args, ct) && (dist - t) > EPS) return true;
+    if (test_ref<CNT>(S, ref, o, d, k, t, args, ct) && (dist - t) > EPS) return true;
   }
   return false;
 }
 template <bool CNT>
-DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, uint32_t tsite, double dist, Counters& ct) {
+DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
   if (A.root < 0) {  // leafVals.calcShadowHit: its own box first
     if (!shadow_box<CNT>(A.bmin, A.bmax, ao, ad, dist, ct)) return false;
-    return leaf_any<CNT>(S, ~A.root, A.xf, ao, ad, w, k, tsite, dist, ct);
+    return leaf_any<CNT>(S, ~A.root, A.xf, ao, ad, w, k, dist, ct);
   }
   int32_t stk[BVH_STACK];
   int sp = 0;
@@ -196,7 +196,7 @@ DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const
     bool down = false;
     if (shadow_box<CNT>(nd.lmin, nd.lmax, ao, ad, dist, ct)) {
       if (nd.left < 0) {
-        if (leaf_any<CNT>(S, ~nd.left, A.xf, ao, ad, w, k, tsite, dist, ct)) return true;
+        if (leaf_any<CNT>(S, ~nd.left, A.xf, ao, ad, w, k, dist, ct)) return true;
       } else {
         N = nd.left;
         down = true;
@@ -208,7 +208,7 @@ DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const
       const NodeD& pn = S.node[stk[--sp]];
       if (shadow_box<CNT>(pn.rmin, pn.rmax, ao, ad, dist, ct)) {
         if (pn.right < 0) {
-          if (leaf_any<CNT>(S, ~pn.right, A.xf, ao, ad, w, k, tsite, dist, ct)) return true;
+          if (leaf_any<CNT>(S, ~pn.right, A.xf, ao, ad, w, k, dist, ct)) return true;
           continue;
         }
         N = pn.right;
@@ -219,7 +219,7 @@ DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const
 }
 // myScene.calcShadow (myScene.java:879-885)
 template <bool CNT>
-DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, uint32_t tsite, double dist, Counters& ct) {
+DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters& ct) {
   for (int i = 0; i < S.ntop; ++i) {
     TopD tp = S.top[i];
     if (CNT) ct.c[C_TOP]++;
@@ -229,12 +229,12 @@ DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, uint32_t tsite, doubl
     if (tp.kind == TOP_ACCEL) {
       if (CNT) ct.c[C_ROOT]++;
       w.moved = false;
-      if (accel_any<CNT>(S, S.accel[tp.idx], o, d, w, k, tsite, dist, ct)) return true;
+      if (accel_any<CNT>(S, S.accel[tp.idx], o, d, w, k, dist, ct)) return true;
     } else {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
       int args;
-      if (test_ref<CNT>(S, ref, o, d, k, tsite, t, args, ct) && (dist - t) > EPS) return true;
+      if (test_ref<CNT>(S, ref, o, d, k, t, args, ct) && (dist - t) > EPS) return true;
     }
   }
   return false;
@@ -261,7 +261,7 @@ DEVI HitRec make_hit(const SceneD& S, const Best& b, V wo, const Key& k) {
   int args = 0;
   double tt;
   Counters dummy;
-  test_ref<false>(S, ref, h.tro, h.trd, k, SITE_TIME, tt, args, dummy);  // recompute args (deterministic)
+  test_ref<false>(S, ref, h.tro, h.trd, k, tt, args, dummy);  // recompute args (deterministic)
   h.args = args;
   V p = mk(h.trd.x * t + h.tro.x, h.trd.y * t + h.tro.y, h.trd.z * t + h.tro.z);
   h.hitLoc = p;
@@ -346,7 +346,7 @@ DEVI V image_color(const SceneD& S, const HitRec& h, const Key& k, const TexD& T
   V p = h.hitLoc;
   if (h.type == PT_SPHERE || h.type == PT_MSPHERE) {  // mySphere.findTextureU/V (myImpObject.java:97-122)
     const PrimD& P = S.prim[~h.ref];
-    V to = sphere_center(P, k, SITE_TIME);
+    V to = sphere_center(P, k);
     double a0 = p.y - to.y, a1 = a0 / P.a[4];
     a1 = (a1 > 1) ? 1 : (a1 < -1) ? -1 : a1;
     v = (T.h - 1) * acos(a1) / PI_D;
@@ -610,7 +610,9 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     }
     if (ltMult == 0) continue;
     if (CNT) ct.c[C_SHADOW]++;
-    if (shadowed<CNT>(S, sr, k, SITE_SHADOW_TIME + li, t, ct)) continue;
+    Key sk = k;
+    sk.tsite = SITE_SHADOW_TIME + li;
+    if (shadowed<CNT>(S, sr, sk, t, ct)) continue;
     renorm(sr);  // shadowRay.direction._normalize()
     double ldp = dot(sr.d, h.nrm) * ltMult;
     if (ldp > EPS) {
@@ -656,6 +658,59 @@ struct Child {  // outgoing ray
   int32_t gen;
 };
 
+// Fresnel split shared by calcTransClr (myObjShader.java:157-276), calcTransRay
+// (:297-397, photons) and the simple shader's calcSimpleTransClr (:503-631).
+struct TransOut {
+  V refr, refl;  // refraction dir; reflection dir (already x refractNormMult)
+  double omtr, tr;
+  bool doA, doB;
+};
+DEVI TransOut trans_split(const MatD& m, const HitRec& h, const double* inKt, bool strans) {
+  TransOut T;
+  V back = mk(h.dw.x * -1, h.dw.y * -1, h.dw.z * -1);
+  V N = h.nrm;
+  double cos1 = dot(back, N), rnm = 1.0;
+  if (cos1 < EPS) { rnm = -1.0; N = mk(N.x * -1, N.y * -1, N.z * -1); }
+  cos1 = dot(back, N);
+  double mb = mag(back), mn = mag(N);
+  double thetaI = acos(dot(back, N) / (mb * mn));  // _angleBetween (DistRayTracer.java:445-452)
+  double idx = strans ? m.perm : m.ktrans;
+  double n = 1, n1 = 0, n2 = 0, cos2 = 0, tr = 0, omtr = 1;
+  bool TIR = false;
+  if (rnm < 0) {  // leaving the material
+    double thetaCrit = asin(1.0 / idx);
+    if (thetaI < thetaCrit) {
+      n1 = idx; n2 = 1; n = (n1 / n2);
+      cos2 = sqrt(1.0 - (n * n) * (1.0 - (cos1 * cos1)));
+    } else {
+      tr = 1; omtr = 1 - tr; TIR = true; cos2 = 0;
+    }
+  } else {
+    n1 = strans ? inKt[1] : inKt[0];
+    n2 = idx;
+    n = (n1 / n2);
+    cos2 = sqrt(1.0 - (n * n) * (1.0 - (cos1 * cos1)));
+  }
+  if (!TIR) {  // Fresnel with cos(theta_t) = sqrt(1 - (n1/n2) sin^2) (Q15)
+    double sa = sin(acos(cos1)), rct = sqrt(1.0 - ((n1 / n2) * sa * sa));
+    double a1 = n1 * cos1, b1 = n2 * rct, nd1 = (a1 - b1) / (a1 + b1);
+    double a2 = n1 * rct, b2 = n2 * cos1, nd2 = (a2 - b2) / (a2 + b2);
+    tr = ((nd1 * nd1) + (nd2 * nd2)) / 2.0;
+    omtr = 1 - tr;
+  }
+  T.omtr = omtr;
+  T.tr = tr;
+  T.doA = strans ? (omtr > 0) : (omtr > EPS);
+  T.doB = strans ? (tr > 0) : (tr > EPS);
+  V u = mk(back.x * (n * -1), back.y * (n * -1), back.z * (n * -1));
+  double kk = (n * cos1) - cos2;
+  V nv = mk(N.x * kk, N.y * kk, N.z * kk);
+  T.refr = nrmz(mk(u.x + nv.x, u.y + nv.y, u.z + nv.z));
+  V rd = refl_dir(back, N);
+  T.refl = mk(rd.x * rnm, rd.y * rnm, rd.z * rnm);
+  return T;
+}
+
 // getColorAtPos (myObjShader.java:409-438; simple shader :635-651). Computes the local
 // colour and the children the node spawns.
 template <bool CNT>
@@ -686,56 +741,20 @@ DEVI void shade_node(const SceneD& S, const HitRec& h, const Child& in, const Ke
   bool strans = m.simple && (m.ktrans > 0);
   if (trans || strans) {  // calcTransClr :157-276 / calcSimpleTransClr :503-631
     F.kind = strans ? 2 : 1;
-    V N = h.nrm;
-    double cos1 = dot(back, N), rnm = 1.0;
-    if (cos1 < EPS) { rnm = -1.0; N = mk(N.x * -1, N.y * -1, N.z * -1); }
-    cos1 = dot(back, N);
-    double mb = mag(back), mn = mag(N);
-    double thetaI = acos(dot(back, N) / (mb * mn));
-    double idx = strans ? m.perm : m.ktrans;
-    double n = 1, n1 = 0, n2 = 0, cos2 = 0, tr = 0, omtr = 1;
-    bool TIR = false;
-    V reflS = strans ? refl_dir(back, N) : mk(0, 0, 0);
-    if (rnm < 0) {
-      double thetaCrit = asin(1.0 / idx);
-      if (thetaI < thetaCrit) {
-        n1 = idx; n2 = 1; n = (n1 / n2);
-        cos2 = sqrt(1.0 - (n * n) * (1.0 - (cos1 * cos1)));
-      } else {
-        tr = 1; omtr = 1 - tr; TIR = true; cos2 = 0;
-      }
-    } else {
-      n1 = strans ? in.kt[1] : in.kt[0];
-      n2 = idx;
-      n = (n1 / n2);
-      cos2 = sqrt(1.0 - (n * n) * (1.0 - (cos1 * cos1)));
-    }
-    if (!TIR) {
-      double sa = sin(acos(cos1)), rct = sqrt(1.0 - ((n1 / n2) * sa * sa));
-      double a1 = n1 * cos1, b1 = n2 * rct, nd1 = (a1 - b1) / (a1 + b1);
-      double a2 = n1 * rct, b2 = n2 * cos1, nd2 = (a2 - b2) / (a2 + b2);
-      tr = ((nd1 * nd1) + (nd2 * nd2)) / 2.0;
-      omtr = 1 - tr;
-    }
-    bool doA = strans ? (omtr > 0) : (omtr > EPS);
-    bool doB = strans ? (tr > 0) : (tr > EPS);
-    if (doA) {
-      V u = mk(back.x * (n * -1), back.y * (n * -1), back.z * (n * -1));
-      double kk = (n * cos1) - cos2;
-      V nv = mk(N.x * kk, N.y * kk, N.z * kk);
-      F.dA = nrmz(mk(u.x + nv.x, u.y + nv.y, u.z + nv.z));
+    TransOut T = trans_split(m, h, in.kt, strans);
+    if (T.doA) {
+      F.dA = T.refr;
       F.hasA = 1;
-      if (strans) { double w = omtr * m.ktrans; F.wA = mk(w, w, w); }
-      else F.wA = mk((omtr) * m.permclr[0], (omtr) * m.permclr[1], (omtr) * m.permclr[2]);
+      if (strans) { double w = T.omtr * m.ktrans; F.wA = mk(w, w, w); }
+      else F.wA = mk((T.omtr) * m.permclr[0], (T.omtr) * m.permclr[1], (T.omtr) * m.permclr[2]);
     }
     F.ktA[0] = m.ktrans; F.ktA[1] = m.perm; F.ktA[2] = m.permclr[0]; F.ktA[3] = m.permclr[1]; F.ktA[4] = m.permclr[2];
-    if (doB) {
-      V rd = strans ? reflS : refl_dir(back, N);
-      F.dB = mk(rd.x * rnm, rd.y * rnm, rd.z * rnm);
+    if (T.doB) {
+      F.dB = T.refl;
       F.hasB = 1;
       F.ktBdefault = strans ? 1 : 0;
-      if (strans) { double w = tr * m.krefl; F.wB = mk(w, w, w); }
-      else F.wB = mk((tr) * m.permclr[0], (tr) * m.permclr[1], (tr) * m.permclr[2]);
+      if (strans) { double w = T.tr * m.krefl; F.wB = mk(w, w, w); }
+      else F.wB = mk((T.tr) * m.permclr[0], (T.tr) * m.permclr[1], (T.tr) * m.permclr[2]);
     }
   } else if (m.krefl > 0.0) {  // calcReflClr :278-294
     V rd = refl_dir(back, h.nrm);
@@ -842,6 +861,7 @@ __global__ void __launch_bounds__(64) render_kernel(SceneD S, ParamsD P, float* 
     Key k;
     k.seed = P.seed;
     k.pixel = (uint64_t)row * (uint64_t)P.W + (uint64_t)col;
+    k.tsite = SITE_TIME;
     V c;
     const int n = P.spp;
     if (S.dof) {  // shootMultiDpthOfFldRays (myScene.java:1386-1406)
@@ -909,6 +929,203 @@ __global__ void __launch_bounds__(64) render_kernel(SceneD S, ParamsD P, float* 
     for (int i = 0; i < C_N; ++i)
       if (ct.c[i]) atomicAdd(&gcount[i], (unsigned long long)ct.c[i]);
   }
+}
+
+// ---------------------------------------------------------------------------
+// photon pre-pass (myScene.sendCausticPhotons :952-998 / sendDiffusePhotons :1000-1091):
+// one lane per emitted photon (light-major, photon index minor). Each lane writes
+// its stored photons into PH_SLOTS slots in path order; the host compacts them in
+// (light, index, slot) order -- the reference's photon_list insertion order.
+static constexpr int PH_SLOTS = 6;
+static constexpr int PH_MAXTRY = 4096;  // rejection-sampling cap (reached with probability ~0)
+struct PhotonOut {
+  double pos[3];
+  double pwr[3];
+};
+DEVI V rot_axis(V v1, V u, double thet) {  // rotVecAroundAxis (DistRayTracer.java:336-349)
+  double cT = cos(thet), sT = sin(thet), oneMC = 1 - cT, ux2 = u.x * u.x, uy2 = u.y * u.y, uz2 = u.z * u.z,
+         uxy = u.x * u.y, uxz = u.x * u.z, uyz = u.y * u.z, uzS = u.z * sT, uyS = u.y * sT, uxS = u.x * sT,
+         uxzC1 = uxz * oneMC, uxyC1 = uxy * oneMC, uyzC1 = uyz * oneMC;
+  return mk((ux2 * oneMC + cT) * v1.x + (uxyC1 - uzS) * v1.y + (uxzC1 + uyS) * v1.z,
+            (uxyC1 + uzS) * v1.x + (uy2 * oneMC + cT) * v1.y + (uyzC1 - uxS) * v1.z,
+            (uxzC1 - uyS) * v1.x + (uyzC1 + uxS) * v1.y + (uz2 * oneMC + cT) * v1.z);
+}
+// genRndPhtnRay (myLight.java:104-107 point, :165-185 spot, :229-242 disk; getRandDir :59-74)
+DEVI void photon_ray(const LightD& L, uint64_t seed, uint64_t i, V& o, V& d) {
+  uint32_t k = 0, li = (uint32_t)L.index;
+  if (L.type == 0) {
+    double x, y, z, sq;
+    int tries = 0;
+    do {
+      x = rng(seed, i, li, 0, SITE_PH_DIR, k++, -1.0, 1.0);
+      y = rng(seed, i, li, 0, SITE_PH_DIR, k++, -1.0, 1.0);
+      z = rng(seed, i, li, 0, SITE_PH_DIR, k++, -1.0, 1.0);
+      sq = (x * x) + (y * y) + (z * z);
+    } while (((sq > 1.0) || (sq < EPS)) && ++tries < PH_MAXTRY);
+    double m = sqrt(sq);
+    d = mk(x / m, y / m, z / m);
+    o = xpt(L.g, ld3(L.origin));
+    return;
+  }
+  if (L.type == 1) {
+    double checkProb = rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, 1), angle, prob;
+    int tries = 0;
+    do {
+      angle = rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, L.outerRad);
+      prob = (angle < L.innerRad) ? 1 : (angle > L.outerRad) ? 0 : (L.outerRad - angle) / L.radDiff;
+    } while (prob > checkProb && ++tries < PH_MAXTRY);
+    V t = nrmz(rot_axis(ld3(L.orient), ld3(L.tangent), angle));
+    d = rot_axis(t, ld3(L.orient), rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, TWO_PI_F));
+    o = xpt(L.g, ld3(L.origin));
+    return;
+  }
+  double angle, prob;
+  int tries = 0;
+  do {
+    angle = rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, PI_D);
+    prob = (angle < 0) ? 1 : (angle > PI_D) ? 0 : (PI_D - angle) / PI_D;
+  } while (prob > rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, 1) && ++tries < PH_MAXTRY);
+  V dd = nrmz(rot_axis(ld3(L.orient), ld3(L.tangent), angle));
+  d = rot_axis(dd, ld3(L.orient), rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, TWO_PI_F));
+  Key kk;
+  kk.seed = seed; kk.pixel = i; kk.sample = li; kk.node = 0; kk.tsite = SITE_PH_TIME;
+  o = xpt(L.g, disk_pos(L, kk, 0));
+}
+// findCausticRayHit (myObjShader.java:461-478) with calcTransRay / calcReflRay
+DEVI bool caustic_ray(const SceneD& S, const HitRec& h, const double* inKt, int gen, double pwr[3], Child& out) {
+  const MatD& m = S.mat[h.mat];
+  if (!((gen < 4) && m.hasCaustic)) return false;  // numPhotonRays = 4
+  double pm[3] = {1.0, 1.0, 1.0};
+  bool ok = false;
+  if ((m.ktrans > 0.0) || (m.perm > 0.0)) {
+    pm[0] = m.phtnPermClr[0]; pm[1] = m.phtnPermClr[1]; pm[2] = m.phtnPermClr[2];
+    TransOut T = trans_split(m, h, inKt, false);
+    out.d = (T.omtr > EPS) ? T.refr : T.refl;
+    out.kt[0] = m.ktrans; out.kt[1] = m.perm; out.kt[2] = m.permclr[0]; out.kt[3] = m.permclr[1]; out.kt[4] = m.permclr[2];
+    ok = true;
+  } else if (m.krefl > 0.0) {
+    pm[0] = pm[1] = pm[2] = m.krefl;
+    out.d = refl_dir(mk(h.dw.x * -1, h.dw.y * -1, h.dw.z * -1), h.nrm);
+    for (int c = 0; c < 5; ++c) out.kt[c] = 1;
+    ok = true;
+  }
+  for (int c = 0; c < 3; ++c) pwr[c] = pwr[c] * pm[c];
+  out.o = h.fwd;
+  out.gen = gen + 1;
+  return ok;
+}
+
+__global__ void __launch_bounds__(64) photon_kernel(SceneD S, uint64_t seed, int numCast, int caustic, double pwrMult,
+                                                   PhotonOut* __restrict__ out, int* __restrict__ cnt) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)S.nlight * numCast) return;
+  const int li = (int)(gid / numCast);
+  const uint64_t i = (uint64_t)(gid % numCast);
+  const LightD& L = S.light[li];
+  Counters ct;
+  int n = 0;
+  PhotonOut* slot = out + gid * PH_SLOTS;
+  double pwr[3] = {L.color[0] * pwrMult, L.color[1] * pwrMult, L.color[2] * pwrMult};
+  Key k;
+  k.seed = seed; k.pixel = i; k.sample = (uint32_t)li; k.node = 0; k.tsite = SITE_PH_TIME;
+  WRay w;
+  photon_ray(L, seed, i, w.o, w.d);
+  w.d = nrmz(w.d);
+  w.stable = false; w.moved = false;
+  double kt[5] = {1, 1, 1, 1, 1};
+  int gen = 0;
+  Best b = closest<false>(S, w, k, ct);
+  if (b.t == DMAX) { cnt[gid] = 0; return; }
+  HitRec h = make_hit(S, b, w.o, k);
+  if (caustic) {
+    if (!S.mat[h.mat].hasCaustic) { cnt[gid] = 0; return; }
+    int rgen = 0;
+    bool hit = true;
+    do {
+      Child c;
+      double cur[3] = {pwr[0], pwr[1], pwr[2]};
+      if (caustic_ray(S, h, kt, gen, cur, c)) {
+        for (int q = 0; q < 3; ++q) pwr[q] = cur[q];
+        for (int q = 0; q < 5; ++q) kt[q] = c.kt[q];
+        rgen = c.gen;
+        k.node = (uint32_t)rgen;
+        w.o = c.o; w.d = nrmz(c.d); w.stable = false; w.moved = false;
+        b = closest<false>(S, w, k, ct);
+        hit = b.t != DMAX;
+        if (hit) { h = make_hit(S, b, w.o, k); gen = rgen; }
+      } else {
+        hit = false;
+      }
+    } while (hit && S.mat[h.mat].hasCaustic && rgen <= 4);
+    if (hit && rgen <= 4) {
+      for (int q = 0; q < 3; ++q) { slot[0].pos[q] = (&h.fwd.x)[q]; slot[0].pwr[q] = pwr[q]; }
+      n = 1;
+    }
+    cnt[gid] = n;
+    return;
+  }
+  bool done = false, firstDiff = true, hit = true;
+  uint32_t bounce = 0;
+  do {
+    bounce++;
+    const MatD& m = S.mat[h.mat];
+    if (m.krefl == 0) {
+      double prob = 0;
+      uint32_t kk = 0;
+      if (!firstDiff) {
+        if (n < PH_SLOTS) {
+          for (int q = 0; q < 3; ++q) { slot[n].pos[q] = (&h.fwd.x)[q]; slot[n].pwr[q] = pwr[q]; }
+          n++;
+        }
+        prob = rng(seed, i, (uint32_t)li, bounce, SITE_PH_BOUNCE, kk++, 0, 1.0);
+      }
+      firstDiff = false;
+      if (prob < m.avgDiffClr) {
+        double x = 0, y = 0, sq;
+        int tries = 0;
+        do {
+          x = rng(seed, i, (uint32_t)li, bounce, SITE_PH_BOUNCE, kk++, -1.0, 1.0);
+          y = rng(seed, i, (uint32_t)li, bounce, SITE_PH_BOUNCE, kk++, -1.0, 1.0);
+          sq = (x * x) + (y * y);
+        } while (((sq >= 1.0) || (sq < EPS)) && ++tries < PH_MAXTRY);
+        double z = sqrt(1 - (sq));
+        V nn = h.nrm;
+        double nx = nn.x * nn.x, ny = nn.y * nn.y, nz = nn.z * nn.z;
+        V tv = ((nx > ny) && (nx > nz)) ? mk(0, 0, 1) : mk(1, 0, 0);
+        V p_ = cross(nn, tv), q_ = cross(p_, nn);
+        nn = mk(nn.x * z, nn.y * z, nn.z * z);
+        p_ = mk(p_.x * x, p_.y * x, p_.z * x);
+        q_ = mk(q_.x * y, q_.y * y, q_.z * y);
+        V bd = nrmz(mk(nn.x + p_.x + q_.x, nn.y + p_.y + q_.y, nn.z + p_.z + q_.z));
+        for (int q = 0; q < 3; ++q) pwr[q] = pwr[q] * m.phtnDiffScl[q];
+        gen = gen + 1;
+        k.node = bounce;
+        w.o = h.fwd; w.d = nrmz(bd); w.stable = false; w.moved = false;
+        for (int q = 0; q < 5; ++q) kt[q] = 1;
+        b = closest<false>(S, w, k, ct);
+        hit = b.t != DMAX;
+        if (hit) h = make_hit(S, b, w.o, k);
+      } else {
+        done = true;
+      }
+    } else {
+      Child c;
+      double cur[3] = {pwr[0], pwr[1], pwr[2]};
+      if (caustic_ray(S, h, kt, gen, cur, c)) {
+        for (int q = 0; q < 3; ++q) pwr[q] = cur[q];
+        for (int q = 0; q < 5; ++q) kt[q] = c.kt[q];
+        gen = c.gen;
+        k.node = bounce;
+        w.o = c.o; w.d = nrmz(c.d); w.stable = false; w.moved = false;
+        b = closest<false>(S, w, k, ct);
+        hit = b.t != DMAX;
+        if (hit) h = make_hit(S, b, w.o, k);
+      } else {
+        hit = false;
+      }
+    }
+  } while (hit && !done && gen <= 4);
+  cnt[gid] = n;
 }
 
 }  // namespace dv
@@ -986,7 +1203,7 @@ static int upload_scene(rt_scene* s) {
   return RT_OK;
 }
 
-int rt_upload_photons(rt_scene* s) {  // called by photon.cpp after the host build
+int rt_upload_photons(rt_scene* s) {  // after the host kd-tree build
   HostScene& h = s->hs;
   HIPCHK(hipSetDevice(s->device));
   int rc = upload(s, h.photon, &s->dev.photon);
@@ -1168,3 +1385,46 @@ int rt_time_render(rt_scene* s, const rt_render_params* p, int warmup, int iters
 }
 
 }  // extern "C"
+
+int rt_upload_photons(rt_scene* s);
+extern "C" int rt_photons_build(rt_scene* s, uint64_t seed) {
+  if (!s) return set_error(RT_E_INVALID, "null scene");
+  HostScene& h = s->hs;
+  if (h.photonMode == 0 || s->photonsUploaded) return RT_OK;
+  if (h.photonCount <= 0 || h.photonK <= 0) return set_error(RT_E_INVALID, "bad photon parameters");
+  if (h.photonK > dv::KNN_MAX) return set_error(RT_E_INVALID, "photon neighbourhood k > 256 unsupported");
+  HIPCHK(hipSetDevice(s->device));
+  const long total = (long)h.light.size() * h.photonCount;
+  std::vector<int> cnt(total > 0 ? total : 1);
+  std::vector<dv::PhotonOut> out;
+  if (total > 0) {
+    dv::PhotonOut* d_out = nullptr;
+    int* d_cnt = nullptr;
+    HIPCHK(hipMalloc(&d_out, sizeof(dv::PhotonOut) * dv::PH_SLOTS * total));
+    HIPCHK(hipMalloc(&d_cnt, sizeof(int) * total));
+    bool caustic = h.photonMode == 2;
+    double pwrMult = (caustic ? 40.0 : 8.0) / h.photonCount;  // causticsLightPwrMult / diffuseLightPwrMult (myScene.java:109-110)
+    long blocks = (total + 63) / 64;
+    hipLaunchKernelGGL(dv::photon_kernel, dim3((unsigned)blocks), dim3(64), 0, 0, s->dev, seed, h.photonCount, caustic ? 1 : 0,
+                       pwrMult, d_out, d_cnt);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(cnt.data(), d_cnt, sizeof(int) * total, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) {
+      out.resize((size_t)dv::PH_SLOTS * total);
+      e = hipMemcpy(out.data(), d_out, sizeof(dv::PhotonOut) * dv::PH_SLOTS * total, hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(d_out);
+    (void)hipFree(d_cnt);
+    if (e != hipSuccess) return set_error(RT_E_HIP, std::string("photon pre-pass: ") + hipGetErrorString(e));
+  }
+  std::vector<double> pos, pwr;
+  for (long g = 0; g < total; ++g)
+    for (int j = 0; j < cnt[g]; ++j) {
+      const dv::PhotonOut& p = out[(size_t)g * dv::PH_SLOTS + j];
+      pos.insert(pos.end(), p.pos, p.pos + 3);
+      pwr.insert(pwr.end(), p.pwr, p.pwr + 3);
+    }
+  build_photon_tree(h, pos, pwr);
+  return rt_upload_photons(s);
+}

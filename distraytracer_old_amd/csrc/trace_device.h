@@ -24,7 +24,7 @@ static constexpr double PI_D = 3.141592653589793;        // Math.PI
 
 enum : uint32_t {
   SITE_AA_Y = 1, SITE_AA_X = 2, SITE_DOF_ANG = 3, SITE_DOF_RAD = 4, SITE_TIME = 8,
-  SITE_DISK = 0x100, SITE_SHADOW_TIME = 0x200
+  SITE_DISK = 0x100, SITE_SHADOW_TIME = 0x200, SITE_PH_DIR = 0x1000, SITE_PH_BOUNCE = 0x1100, SITE_PH_TIME = 0x1200
 };
 enum { C_CAMERA = 0, C_SHADOW, C_REFL, C_REFR, C_BOX, C_TRI, C_QUAD, C_IMPLICIT, C_LIGHT, C_PHOTON, C_TEXEL,
        C_NODE, C_LEAF, C_MEMBER, C_ROOT, C_TOP, C_N = 16 };
@@ -103,6 +103,7 @@ DEVI double rng(uint64_t seed, uint64_t a, uint32_t b, uint32_t c, uint32_t site
 struct Key {
   uint64_t seed, pixel;
   uint32_t sample, node;
+  uint32_t tsite;  // RNG site of per-object ray times (myRay.getTime): camera/secondary, shadow or photon rays
 };
 
 // World ray with the reference's in-place re-normalisation state
@@ -201,16 +202,16 @@ DEVI bool tri_test(const TriD& T, V o, V d, double& t, int& st) {
   return planar_test<3, false>(T.v, nA, nB, T.dA, T.dB, o, d, t, st);
 }
 
-DEVI V sphere_center(const PrimD& P, const Key& k, uint32_t site) {
+DEVI V sphere_center(const PrimD& P, const Key& k) {
   if (P.type != PT_MSPHERE) return ld3(P.a);
   // myMovingSphere.getOrigin(ray.getTime()) : keyed per (ray, object)
-  double tm = rng(k.seed, k.pixel, k.sample, k.node, site, P.key, 0, 1.0);
+  double tm = rng(k.seed, k.pixel, k.sample, k.node, k.tsite, P.key, 0, 1.0);
   V o0 = ld3(P.a), o1 = ld3(P.a + 6);
   V bMa = sub(o1, o0);
   return mk(o0.x + tm * bMa.x, o0.y + tm * bMa.y, o0.z + tm * bMa.z);
 }
 
-DEVI bool prim_test(const PrimD& P, V o, V d, const Key& k, uint32_t tsite, double& t, int& args) {
+DEVI bool prim_test(const PrimD& P, V o, V d, const Key& k, double& t, int& args) {
   switch (P.type) {
     case PT_QUAD:
     case PT_PLANE: {
@@ -221,7 +222,7 @@ DEVI bool prim_test(const PrimD& P, V o, V d, const Key& k, uint32_t tsite, doub
     }
     case PT_SPHERE:
     case PT_MSPHERE: {  // mySphere.intersectCheck (myImpObject.java:76-94)
-      V c = sphere_center(P, k, tsite);
+      V c = sphere_center(P, k);
       double rx = P.a[3], ry = P.a[4], rz = P.a[5];
       double a = ((d.x / rx) * (d.x / rx)) + ((d.y / ry) * (d.y / ry)) + ((d.z / rz) * (d.z / rz));
       V pC = mk((o.x - c.x) / rx, (o.y - c.y) / ry, (o.z - c.z) / rz);

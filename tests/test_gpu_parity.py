@@ -94,3 +94,22 @@ def test_ray_counts_match_oracle():
     _, _, so = o.render(128, 128, spp=2, seed=SEED)
     for k in ("camera", "shadow", "refl", "refr", "tri", "light"):
         assert abs(sg[k] - so[k]) <= 1e-3 * max(1, so[k]), (k, sg[k], so[k])
+
+
+@pytest.mark.parametrize("mode,spec", [("diffuse", "diffuse_photons  20000  50 0.1"),
+                                       ("caustic", "caustic_photons  20000  40 0.05")])
+def test_photon_map_parity(tmp_path, mode, spec):
+    """C5 path (t11 Cornell box): GPU photon shooting + kd-tree + kNN gather vs the oracle, with a
+    reduced photon count so the oracle finishes in seconds."""
+    src = (scenes.SCENE_DIR / "t11.cli").read_text().replace("diffuse_photons  1000000  200 0.1", spec)
+    (tmp_path / "t11s.cli").write_text(src)
+    g = rt.Scene.load_cli("t11s.cli", scene_dir=tmp_path, textures={})
+    o = OracleScene(tmp_path, "t11s.cli")
+    seed = 0x5EED0005
+    g.build_photons(seed)
+    n_o = o.build_photons(seed)
+    assert g.info()["photons"] == n_o
+    rg, ag = g.render(64, 64, spp=2, seed=seed)
+    ro, ao, _ = o.render(64, 64, spp=2, seed=seed)
+    c = compare(rg, ag, ro, ao)
+    assert c["mismatch_frac"] < 5e-3, c
