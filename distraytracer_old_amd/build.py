@@ -15,7 +15,7 @@ LIB_DIR = PKG / "lib"
 LIB_PATH = LIB_DIR / "libdistraytracer.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["trace.hip", "cli_loader.cpp", "scene_build.cpp", "photon.cpp"]
-HEADERS = ["rt_types.h", "rt_internal.h", "host_math.h", "trace_device.h"]
+HEADERS = ["rt_types.h", "rt_internal.h", "host_math.h", "trace_device.h", "trace_kernels.h"]
 # -ffp-contract=off: keep the reference's (Java) unfused double arithmetic so discrete
 # decisions (hits, shadows, TIR) match the oracle; no fast-math (IEEE Inf/NaN needed).
 COMPILE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
@@ -30,16 +30,19 @@ def _stale() -> bool:
     return any(p.stat().st_mtime > t for p in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, defines: list[str] | None = None, out: Path | None = None) -> Path:
+    """Build the library (in-tree). `defines`/`out`: tuning experiments (tools/variant_sweep.py)."""
+    target = Path(out) if out else LIB_PATH
+    if not force and not defines and out is None and not _stale():
         return LIB_PATH
-    LIB_DIR.mkdir(exist_ok=True)
-    tmp = LIB_PATH.with_suffix(".so.tmp%d" % os.getpid())
+    target.parent.mkdir(parents=True, exist_ok=True)
+    tmp = target.with_suffix(".so.tmp%d" % os.getpid())
     objs, logs = [], []
+    tag = "" if out is None else target.stem + "."
     for src in SOURCES:  # .hip -> device+host; .cpp -> host-only C++ (no device pass)
-        obj = LIB_DIR / (src + ".o")
+        obj = target.parent / (tag + src + ".o")
         lang = [] if src.endswith(".hip") else ["-x", "c++"]
-        cmd = [HIPCC, *COMPILE_FLAGS, *lang, "-c", str(CSRC / src), "-o", str(obj)]
+        cmd = [HIPCC, *COMPILE_FLAGS, *["-D" + d for d in (defines or [])], *lang, "-c", str(CSRC / src), "-o", str(obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         logs.append(r.stderr)
         if r.returncode != 0:
@@ -50,8 +53,8 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         raise RuntimeError("link failed:\n" + r.stderr[-4000:])
     if verbose:
         print("\n".join(logs))
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":

@@ -108,8 +108,11 @@ struct Key {
 
 // World ray with the reference's in-place re-normalisation state
 // (myRay.getTransformedRay normalises the source direction, myRay.java:91-93).
+// `ver` counts the re-normalisations that changed d, so the direction seen by any
+// earlier test is nrmz^ver(d0) and hit candidates need not carry a direction.
 struct WRay {
-  V o, d;
+  V o, d, d0;
+  uint32_t ver;
   bool stable;  // normalize(d) == d
   bool moved;   // d changed since the cached accel-space ray was built
 };
@@ -117,7 +120,7 @@ DEVI void renorm(WRay& r) {
   if (!r.stable) {
     V n = nrmz(r.d);
     r.stable = veq(n, r.d);
-    if (!r.stable) r.moved = true;
+    if (!r.stable) { r.moved = true; r.ver++; }
     r.d = n;
   }
 }

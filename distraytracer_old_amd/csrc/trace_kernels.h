@@ -1,0 +1,1160 @@
+// HIP kernels (gfx950) for the reference's per-pixel / per-sample trace loop.
+// Included by trace.hip only.
+//
+// Kernel structure: one lane per pixel (8x8 pixel tiles per 64-lane wave for
+// ray coherence); per sample: camera ray -> shading tree evaluated post-order
+// with an explicit per-lane frame stack (per-level myColor clamping, Q8, makes
+// throughput-weighted path accumulation incorrect) -> closest hit = linear
+// scan of objList with the reference-order BVH traversal -> lights with any-hit
+// shadow rays -> reflection / refraction children.
+//
+// Every kernel is instantiated per scene-feature mask F (FT_* below): code for
+// features a scene does not use is compiled out, which is what keeps register
+// and scratch use (hence occupancy) low for the common configurations.
+#pragma once
+#include "trace_device.h"
+
+namespace rt {
+namespace dv {
+
+// scene feature mask (host: scene_features())
+enum : uint32_t {
+  FT_PRIM = 1,    // non-triangle primitives (quad/plane/sphere/cylinder/box)
+  FT_TEX = 2,     // image / noise / marble textures or a textured skydome
+  FT_PHOTON = 4,  // photon map gather
+  FT_TRANS = 8,   // transparent materials (Fresnel split, two children per node)
+  FT_DOF = 16,    // lens / depth of field
+  FT_LIGHTX = 32, // spot or disk lights
+  FT_ALL = 63
+};
+
+__constant__ int c_perm[256];
+__constant__ int c_grad3[12][3];
+
+// ---------------------------------------------------------------------------
+// a hit candidate: the world direction at test time is identified by the ray's
+// re-normalisation version (WRay.ver), so no direction vector is carried around
+struct Best {
+  double t;
+  int32_t ref;   // >= 0 tri, < 0 ~prim
+  uint32_t ver;  // direction version at the winning test
+  int16_t top;   // objList index
+  int16_t inAcc; // hit came from an accel structure (reCalcCTMHitNorm applies)
+};
+DEVI Best miss() { Best b; b.t = DMAX; b.ref = 0; b.top = -1; b.ver = 0; b.inAcc = 0; return b; }
+
+template <bool CNT, uint32_t F>
+DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, double& t, int& args, Counters& ct) {
+  if (!(F & FT_PRIM) || ref >= 0) {
+    if (CNT) ct.c[C_TRI]++;
+    return tri_test(S.tri[ref], o, d, t, args);
+  }
+  const PrimD& P = S.prim[~ref];
+  if (CNT) { if (P.type == PT_QUAD || P.type == PT_PLANE) ct.c[C_QUAD]++; else ct.c[C_IMPLICIT]++; }
+  return prim_test(P, o, d, k, t, args);
+}
+template <uint32_t F>
+DEVI int32_t ref_xf(const SceneD& S, int32_t ref) { return (!(F & FT_PRIM) || ref >= 0) ? S.tri[ref].xf : S.prim[~ref].xf; }
+
+// myGeomList.traverseStruct leaf loop (myGeomBase.java:281-296): strict <, leaf order
+template <bool CNT, uint32_t F>
+DEVI void leaf_closest(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, const Key& k, Best& cur, Counters& ct) {
+  LeafD lf = S.leaf[leaf];
+  if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
+  for (int i = 0; i < lf.count; ++i) {
+    int32_t ref = S.member[lf.start + i];
+    renorm(w);  // _ray.getTransformedRay(_ray, obj.CTMara[invIDX])
+    int xf = ref_xf<F>(S, ref);
+    V o, d;
+    if (xf == accXf && !w.moved) { o = ao; d = ad; }
+    else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
+    double t;
+    int args;
+    if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct) && t < cur.t) {
+      cur.t = t; cur.ref = ref; cur.ver = w.ver;
+    }
+  }
+}
+
+static constexpr int BVH_STACK = 40;  // host rejects BVHs deeper than 40
+
+// myAccelStruct.intersectCheck + myBVH.traverseStruct (myGeomBase.java:216-222, 407-421),
+// iteratively with the reference's LOCAL pruning: the right child is visited iff its
+// box is hit and (left subtree missed or box entry t < the LEFT SUBTREE's best t);
+// ties go left. Each pushed frame saves the enclosing context's best; the right box is
+// tested when the left subtree is done, as the Java does.
+struct TFrame {
+  double savedT;
+  int32_t nodePh;  // node << 1 | phase (0: left subtree in progress, 1: right)
+  int32_t savedRef;
+  uint32_t savedVer;
+};
+template <bool CNT, uint32_t F>
+DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, Best& out, Counters& ct) {
+  Best cur = miss();
+  if (A.root < 0) {
+    leaf_closest<CNT, F>(S, ~A.root, A.xf, ao, ad, w, k, cur, ct);
+  } else {
+    TFrame stk[BVH_STACK];
+    int sp = 0;
+    int32_t N = A.root;
+    while (true) {
+      // descend: push N, go left while the left box is hit
+      while (N >= 0) {
+        const NodeD& nd = S.node[N];
+        if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }  // both child boxes are tested once per visit
+        TFrame& f = stk[sp++];
+        f.nodePh = N << 1;
+        f.savedT = cur.t; f.savedRef = cur.ref; f.savedVer = cur.ver;
+        cur.t = DMAX;
+        double tL;
+        if (slab(nd.lmin, nd.lmax, ao, ad, tL)) N = nd.left;
+        else { N = INT32_MAX; break; }
+      }
+      if (N != INT32_MAX) leaf_closest<CNT, F>(S, ~N, A.xf, ao, ad, w, k, cur, ct);
+      // unwind
+      bool down = false;
+      while (sp > 0) {
+        TFrame& f = stk[sp - 1];
+        if ((f.nodePh & 1) == 0) {
+          const NodeD& nd = S.node[f.nodePh >> 1];
+          double tR;
+          if (slab(nd.rmin, nd.rmax, ao, ad, tR) && (cur.t == DMAX || tR < cur.t)) {
+            f.nodePh |= 1;
+            N = nd.right;
+            down = true;
+            break;
+          }
+        }
+        // node result = cur; merge into the enclosing context (saved wins ties: it is earlier)
+        if (f.savedT <= cur.t) { cur.t = f.savedT; cur.ref = f.savedRef; cur.ver = f.savedVer; }
+        sp--;
+      }
+      if (!down) break;
+    }
+  }
+  if (cur.t != DMAX) { cur.inAcc = 1; out = cur; }
+  else out = miss();
+}
+
+// findClosestRayHit (myScene.java:888-903): objList scan, TreeMap keeps the first of equal t
+template <bool CNT, uint32_t F>
+DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
+  Best best = miss();
+  for (int i = 0; i < S.ntop; ++i) {
+    TopD tp = S.top[i];
+    if (CNT) ct.c[C_TOP]++;
+    renorm(w);
+    const double* inv = S.xf[tp.xf].inv;
+    V o = xpt(inv, w.o), d = xvec(inv, w.d);
+    if (tp.kind == TOP_ACCEL) {
+      const AccelD& A = S.accel[tp.idx];
+      if (CNT) { ct.c[C_ROOT]++; ct.c[C_BOX]++; }
+      double te;
+      if (!slab(A.bmin, A.bmax, o, d, te)) continue;
+      w.moved = false;
+      Best r;
+      accel_closest<CNT, F>(S, A, o, d, w, k, r, ct);
+      if (r.t < best.t) { best = r; best.top = (int16_t)i; }
+    } else {
+      int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
+      double t;
+      int args;
+      if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct) && t < best.t) {
+        best.t = t; best.ref = ref; best.top = (int16_t)i; best.inAcc = 0; best.ver = w.ver;
+      }
+    }
+  }
+  return best;
+}
+
+// any-hit: mySceneObject/myBBox/myGeomList/myBVH.calcShadowHit (mySceneObject.java:33-38,
+// myGeomBase.java:166-170, 268-277, 397-404): blocked iff hit && dist - t > 1e-7
+template <bool CNT>
+DEVI bool shadow_box(const double* mn, const double* mx, V o, V d, double dist, Counters& ct) {
+  if (CNT) ct.c[C_BOX]++;
+  double te;
+  return slab(mn, mx, o, d, te) && (dist - te) > EPS;
+}
+template <bool CNT, uint32_t F>
+DEVI bool leaf_any(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
+  LeafD lf = S.leaf[leaf];
+  if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
+  for (int i = 0; i < lf.count; ++i) {
+    int32_t ref = S.member[lf.start + i];
+    renorm(w);
+    int xf = ref_xf<F>(S, ref);
+    V o, d;
+    if (xf == accXf && !w.moved) { o = ao; d = ad; }
+    else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
+    double t;
+    int args;
+    if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct) && (dist - t) > EPS) return true;
+  }
+  return false;
+}
+template <bool CNT, uint32_t F>
+DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
+  if (A.root < 0) {  // leafVals.calcShadowHit: its own box first
+    if (!shadow_box<CNT>(A.bmin, A.bmax, ao, ad, dist, ct)) return false;
+    return leaf_any<CNT, F>(S, ~A.root, A.xf, ao, ad, w, k, dist, ct);
+  }
+  int32_t stk[BVH_STACK];
+  int sp = 0;
+  int32_t N = A.root;  // internal: no box test of its own (myBVH.calcShadowHit)
+  while (true) {
+    const NodeD& nd = S.node[N];
+    if (CNT) ct.c[C_NODE]++;
+    stk[sp++] = N;  // right child pending
+    bool down = false;
+    if (shadow_box<CNT>(nd.lmin, nd.lmax, ao, ad, dist, ct)) {
+      if (nd.left < 0) {
+        if (leaf_any<CNT, F>(S, ~nd.left, A.xf, ao, ad, w, k, dist, ct)) return true;
+      } else {
+        N = nd.left;
+        down = true;
+      }
+    }
+    if (down) continue;
+    while (true) {
+      if (sp == 0) return false;
+      const NodeD& pn = S.node[stk[--sp]];
+      if (shadow_box<CNT>(pn.rmin, pn.rmax, ao, ad, dist, ct)) {
+        if (pn.right < 0) {
+          if (leaf_any<CNT, F>(S, ~pn.right, A.xf, ao, ad, w, k, dist, ct)) return true;
+          continue;
+        }
+        N = pn.right;
+        break;
+      }
+    }
+  }
+}
+// myScene.calcShadow (myScene.java:879-885)
+template <bool CNT, uint32_t F>
+DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters& ct) {
+  for (int i = 0; i < S.ntop; ++i) {
+    TopD tp = S.top[i];
+    if (CNT) ct.c[C_TOP]++;
+    renorm(w);
+    const double* inv = S.xf[tp.xf].inv;
+    V o = xpt(inv, w.o), d = xvec(inv, w.d);
+    if (tp.kind == TOP_ACCEL) {
+      if (CNT) ct.c[C_ROOT]++;
+      w.moved = false;
+      if (accel_any<CNT, F>(S, S.accel[tp.idx], o, d, w, k, dist, ct)) return true;
+    } else {
+      int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
+      double t;
+      int args;
+      if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct) && (dist - t) > EPS) return true;
+    }
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// hit record (myRay.objHit :119-125, rayHit ctor :147-161, reCalcCTMHitNorm :168-175)
+struct HitRec {
+  V hitLoc, fwd, nrm, dw;
+  int32_t mat, args, type, ref;
+  uint32_t key;
+};
+template <uint32_t F>
+DEVI HitRec make_hit(const SceneD& S, const Best& b, const WRay& w, const Key& k) {
+  HitRec h;
+  int32_t ref = b.ref;
+  V dw = w.d0;  // direction at the winning test: d0 re-normalised `ver` times
+  for (uint32_t i = 0; i < b.ver; ++i) dw = nrmz(dw);
+  int xf, xfc;
+  if (!(F & FT_PRIM) || ref >= 0) { const TriD& T = S.tri[ref]; xf = T.xf; xfc = T.xfc; h.mat = T.mat; h.key = T.key; h.type = PT_TRI; }
+  else { const PrimD& P = S.prim[~ref]; xf = P.xf; xfc = P.xfc; h.mat = P.mat; h.key = P.key; h.type = P.type; }
+  h.ref = ref;
+  const XformD& X = S.xf[xf];
+  V tro = xpt(X.inv, w.o), trd = xvec(X.inv, dw);
+  double t = b.t, tt;
+  int args = 0;
+  Counters dummy;
+  test_ref<false, F>(S, ref, tro, trd, k, tt, args, dummy);  // recompute args (deterministic)
+  h.args = args;
+  V p = mk(trd.x * t + tro.x, trd.y * t + tro.y, trd.z * t + tro.z);
+  h.hitLoc = p;
+  V n;
+  if (!(F & FT_PRIM) || ref >= 0) {  // planar getNormalAtPoint: the stored N, normalised again
+    V nA = ld3(S.tri[ref].n);
+    n = args ? mk(-nA.x, -nA.y, -nA.z) : nA;
+    n = nrmz(n);
+  } else {
+    const PrimD& P = S.prim[~ref];
+    switch (P.type) {
+      case PT_QUAD:
+      case PT_PLANE: n = nrmz(args ? ld3(P.a + 15) : ld3(P.a + 12)); break;
+      case PT_SPHERE:
+      case PT_MSPHERE: {  // getNormalAtPoint uses the static origin (myImpObject.java:68-74)
+        n = nrmz(mk(p.x - P.a[0], p.y - P.a[1], p.z - P.a[2]));
+        if (P.flags & 1) n = mk(n.x * -1.0, n.y * -1.0, n.z * -1.0);
+        break;
+      }
+      case PT_HCYL: {
+        n = (args == 1) ? mk(P.a[0] - p.x, 0, P.a[2] - p.z) : mk(p.x - P.a[0], 0, p.z - P.a[2]);
+        n = nrmz(n);
+        if (P.flags & 1) n = mk(n.x * -1, n.y * -1, n.z * -1);
+        break;
+      }
+      case PT_CYL: {
+        n = (args >= 2) ? mk(p.x - P.a[0], 0, p.z - P.a[2]) : ld3(P.a + 8 + 4 * args);
+        n = nrmz(n);
+        if (P.flags & 1) n = mk(n.x * -1, n.y * -1, n.z * -1);
+        break;
+      }
+      default: {  // box plane normals (myGeomBase.java:175-186)
+        const double tab[7][3] = {{-1, 0, 0}, {0, -1, 0}, {0, 0, -1}, {1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, -1}};
+        int a = (args >= 0 && args < 6) ? args : 6;
+        n = mk(tab[a][0], tab[a][1], tab[a][2]);
+      }
+    }
+  }
+  const XformD& M = (b.inAcc && xfc >= 0) ? S.xf[xfc] : X;  // Q4: accel CTM x object CTM
+  h.fwd = xpt(M.g, p);
+  h.nrm = nrmz(xvec(M.adj, n));
+  h.dw = ((F & FT_PRIM) && h.type == PT_BOX) ? xvec(X.g, trd) : dw;
+  return h;
+}
+
+// ---------------------------------------------------------------------------
+// Perlin noise (float), DistRayTracer.java:234-310
+DEVI int pm(int i) { return c_perm[i & 255]; }
+DEVI int ffl(float x) { return x > 0 ? (int)x : (int)x - 1; }
+DEVI float gd(int g, float x, float y, float z) { return c_grad3[g][0] * x + c_grad3[g][1] * y + c_grad3[g][2] * z; }
+DEVI float fmx(float a, float b, float t) { return (1 - t) * a + t * b; }
+DEVI float fade(float t) { return t * t * t * (t * (t * 6 - 15) + 10); }
+DEVI float noise3(float x, float y, float z) {
+  int X = ffl(x), Y = ffl(y), Z = ffl(z);
+  x = x - X; y = y - Y; z = z - Z;
+  X = X & 255; Y = Y & 255; Z = Z & 255;
+  int g000 = pm(X + pm(Y + pm(Z))) % 12, g001 = pm(X + pm(Y + pm(Z + 1))) % 12;
+  int g010 = pm(X + pm(Y + 1 + pm(Z))) % 12, g011 = pm(X + pm(Y + 1 + pm(Z + 1))) % 12;
+  int g100 = pm(X + 1 + pm(Y + pm(Z))) % 12, g101 = pm(X + 1 + pm(Y + pm(Z + 1))) % 12;
+  int g110 = pm(X + 1 + pm(Y + 1 + pm(Z))) % 12, g111 = pm(X + 1 + pm(Y + 1 + pm(Z + 1))) % 12;
+  float n000 = gd(g000, x, y, z), n100 = gd(g100, x - 1, y, z), n010 = gd(g010, x, y - 1, z), n110 = gd(g110, x - 1, y - 1, z);
+  float n001 = gd(g001, x, y, z - 1), n101 = gd(g101, x - 1, y, z - 1), n011 = gd(g011, x, y - 1, z - 1), n111 = gd(g111, x - 1, y - 1, z - 1);
+  float u = fade(x), v = fade(y), w = fade(z);
+  return fmx(fmx(fmx(n000, n100, u), fmx(n010, n110, u), v), fmx(fmx(n001, n101, u), fmx(n011, n111, u), v), w);
+}
+
+DEVI V texel(const SceneD& S, const TexD& T, long i) {  // myColor(int)
+  long n = (long)T.w * T.h;
+  if (i < 0) i = 0;
+  if (i >= n) i = n - 1;
+  uint32_t c = S.texel[T.off + i];
+  return mk(((c >> 16) & 0xFF) / 255.0, ((c >> 8) & 0xFF) / 255.0, (c & 0xFF) / 255.0);
+}
+DEVI V lerpc(V a, double t, V b) {  // myColor.interpColor (clamped <= 1)
+  return mk(jmin(1, a.x + t * (b.x - a.x)), jmin(1, a.y + t * (b.y - a.y)), jmin(1, a.z + t * (b.z - a.z)));
+}
+
+// myImageTexture.getTextureColor (myTextureHandler.java:84-103) + findTxtrCoords
+template <bool CNT>
+DEVI V image_color(const SceneD& S, const HitRec& h, const Key& k, const TexD& T, Counters& ct) {
+  double u = 0, v = 0;
+  V p = h.hitLoc;
+  if (h.type == PT_SPHERE || h.type == PT_MSPHERE) {  // mySphere.findTextureU/V (myImpObject.java:97-122)
+    const PrimD& P = S.prim[~h.ref];
+    V to = sphere_center(P, k);
+    double a0 = p.y - to.y, a1 = a0 / P.a[4];
+    a1 = (a1 > 1) ? 1 : (a1 < -1) ? -1 : a1;
+    v = (T.h - 1) * acos(a1) / PI_D;
+    double shWm1 = T.w - 1, z1 = p.z - to.z, q = v / (T.h - 1);
+    double b0 = (p.x - to.x) / P.a[3];
+    b0 = (b0 > 1) ? 1 : (b0 < -1) ? -1 : b0;
+    double b1 = sin(q * PI_D);
+    double a2 = (fabs(b1) < EPS) ? 1 : b0 / b1;
+    u = (z1 <= EPS) ? ((shWm1 * acos(a2)) / TWO_PI_F + shWm1 / 2.0) : shWm1 - ((shWm1 * acos(a2)) / TWO_PI_F + shWm1 / 2.0);
+    u = (u < 0) ? 0 : (u > shWm1) ? shWm1 : u;
+  } else if (h.type == PT_TRI || h.type == PT_QUAD || h.type == PT_PLANE) {  // barycentric (myPlanarObject.java:178-186)
+    double vx[4][3], uvv[4][2];
+    int nv = 3;
+    if (h.type == PT_TRI) {
+      const TriD& T3 = S.tri[h.ref];
+      for (int i = 0; i < 3; ++i) { for (int c = 0; c < 3; ++c) vx[i][c] = T3.v[i][c]; uvv[i][0] = 0; uvv[i][1] = 0; }
+    } else {
+      const PrimD& P = S.prim[~h.ref];
+      nv = 4;
+      for (int i = 0; i < 4; ++i) { for (int c = 0; c < 3; ++c) vx[i][c] = P.a[3 * i + c]; uvv[i][0] = P.a[20 + 2 * i]; uvv[i][1] = P.a[21 + 2 * i]; }
+    }
+    double w[4][3], wu[4][2];
+    for (int i = 0; i < nv; ++i) {
+      int s = h.args ? nv - 1 - i : i;
+      for (int c = 0; c < 3; ++c) w[i][c] = vx[s][c];
+      wu[i][0] = uvv[s][0]; wu[i][1] = uvv[s][1];
+    }
+    V P2P0 = mk(w[1][0] - w[0][0], w[1][1] - w[0][1], w[1][2] - w[0][2]);
+    V P2P2 = (nv == 3) ? mk(w[0][0] - w[2][0], w[0][1] - w[2][1], w[0][2] - w[2][2])
+                       : mk(w[3][0] - w[2][0], w[3][1] - w[2][1], w[3][2] - w[2][2]);
+    double d0 = dot(P2P0, P2P0), d2 = dot(P2P2, P2P2), dn = -dot(P2P0, P2P2);
+    double bary = 1.0 / ((d0 * d2) - (dn * dn));
+    V Pm0 = mk(P2P2.x * -1.0, P2P2.y * -1.0, P2P2.z * -1.0);
+    V v2 = sub(p, ld3(w[0]));
+    double dot20 = dot(v2, P2P0), dot21 = dot(v2, Pm0);
+    double cu = ((d2 * dot20) - (dn * dot21)) * bary, cv = ((d0 * dot21) - (dn * dot20)) * bary, cw = 1 - cu - cv;
+    double uu = wu[0][0] * cw + wu[1][0] * cu + wu[2][0] * cv, vv = wu[0][1] * cw + wu[1][1] * cu + wu[2][1] * cv;
+    u = uu * (T.w - 1);
+    v = (1 - vv) * (T.h - 1);
+  }
+  if (CNT) ct.c[C_TEXEL]++;
+  int ui = jd2i(u), vi = jd2i(v);
+  long i00 = (long)vi * T.w + ui, i10 = i00 + T.w, i01 = i00 + 1, i11 = i10 + 1;
+  V c00 = texel(S, T, i00), c10 = texel(S, T, i10), c01 = texel(S, T, i01), c11 = texel(S, T, i11);
+  double fu = u - ui, fv = v - vi;
+  V c0 = lerpc(c00, fu, c01), c1 = lerpc(c10, fu, c11);
+  return lerpc(c0, fv, c1);
+}
+
+// getDiffTxtrColor of the shader's texture handler (myTextureHandler.java)
+template <bool CNT, uint32_t F>
+DEVI V diff_color(const SceneD& S, const MatD& m, const HitRec& h, const Key& k, double diffConst, Counters& ct) {
+  if constexpr ((F & FT_TEX) != 0) {
+    if (m.tex == 1) {  // myImageTexture :105-117
+      V c = (m.texTop >= 0) ? image_color<CNT>(S, h, k, S.tex[m.texTop], ct) : ld3(m.diffuse);
+      return mk(c.x * diffConst, c.y * diffConst, c.z * diffConst);
+    }
+    if (m.tex == 2 || m.tex == 4) {
+      V hv = m.useFwdTrans ? h.fwd : h.hitLoc;
+      hv = mk(hv.x * m.scale, hv.y * m.scale, hv.z * m.scale);
+      V out;
+      if (m.tex == 2) {  // myNoiseTexture :257-265
+        double res = m.turbMult * noise3((float)hv.x, (float)hv.y, (float)hv.z);
+        double val = .5 * res + .5;
+        out = mk(val, val, val);
+      } else {  // myMarbleTexture :366-377 with getAbsTurbVal :242-251 and getClrAra :277-294
+        double res = 0, fs = 1.0, as = 1.0;
+        for (int i = 0; i < m.octaves; ++i) {
+          res += fabs(noise3((float)(hv.x * fs), (float)(hv.y * fs), (float)(hv.z * fs))) * as;
+          as *= .5;
+          fs *= 1.92;
+        }
+        double lin = (hv.x * m.periodMult[0] + hv.y * m.periodMult[1] + hv.z * m.periodMult[2]);
+        double spt = lin / m.pmMag + m.turbMult * res;
+        double dv = .5 * sin(spt) + .5;
+        V pt = mk(hv.x * m.colorScale, hv.y * m.colorScale, hv.z * m.colorScale);
+        double rm0 = 1.0, rm1 = 1.0, rm2 = 1.0;
+        if (m.rndColors) {
+          rm0 = 1.0 + (m.colorMult * noise3((float)pt.x, (float)pt.z, (float)pt.y));
+          rm1 = 1.0 + (m.colorMult * noise3((float)pt.y, (float)pt.x, (float)pt.z));
+          rm2 = 1.0 + (m.colorMult * noise3((float)pt.z, (float)pt.y, (float)pt.x));
+        }
+        const double* c0 = m.colors[0];
+        const double* c1 = m.colors[1];
+        out = mk(jmax(0, jmin(1.0, (c0[0]) + rm0 * dv * ((c1[0]) - (c0[0])))),
+                 jmax(0, jmin(1.0, (c0[1]) + rm1 * dv * ((c1[1]) - (c0[1])))),
+                 jmax(0, jmin(1.0, (c0[2]) + rm2 * dv * ((c1[2]) - (c0[2])))));
+      }
+      if (fabs(diffConst - 1.0) > EPS) out = mk(out.x * diffConst, out.y * diffConst, out.z * diffConst);
+      return out;
+    }
+  }
+  return mk(m.diffuse[0] * diffConst, m.diffuse[1] * diffConst, m.diffuse[2] * diffConst);  // myNonTexture
+}
+
+// photon kNN gather: myKD_Tree.find_near / findNearbyNodes (myLight.java:389-445) and
+// getIrradianceFromPhtnTree (myObjShader.java:441-458). Exact k nearest within r_max with
+// a shrinking radius; the per-lane max-heap lives in scratch.
+static constexpr int KNN_MAX = 256;
+template <bool CNT>
+DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
+  if (S.photonRoot < 0) return mk(0, 0, 0);
+  double hd[KNN_MAX];
+  int32_t hi[KNN_MAX];
+  int hn = 0;
+  const int K = S.photonK < KNN_MAX ? S.photonK : KNN_MAX;
+  double maxd2 = S.photonMaxD2;
+  double pos[3] = {p.x, p.y, p.z};
+  int32_t stN[64];
+  uint8_t stS[64];
+  int sp = 0;
+  stN[0] = S.photonRoot; stS[0] = 0; sp = 1;
+  while (sp > 0) {
+    int32_t ni = stN[sp - 1];
+    const PhotonD& ph = S.photon[ni];
+    uint8_t state = stS[sp - 1];
+    if (state == 0) {
+      if (CNT) ct.c[C_PHOTON]++;
+      stS[sp - 1] = 1;
+      if (ph.axis != -1) {
+        double delta = pos[ph.axis] - ph.pos[ph.axis];
+        int32_t nearC = delta < 0 ? ph.left : ph.right;
+        if (nearC != -1 && sp < 64) { stN[sp] = nearC; stS[sp] = 0; sp++; }
+      }
+      continue;
+    }
+    if (state == 1) {
+      stS[sp - 1] = 2;
+      if (ph.axis != -1) {
+        double delta = pos[ph.axis] - ph.pos[ph.axis], delta2 = delta * delta;
+        int32_t farC = delta < 0 ? ph.right : ph.left;
+        if (farC != -1 && delta2 < maxd2 && sp < 64) { stN[sp] = farC; stS[sp] = 0; sp++; }
+      }
+      continue;
+    }
+    sp--;
+    double dx = pos[0] - ph.pos[0], dy = pos[1] - ph.pos[1], dz = pos[2] - ph.pos[2];
+    double len2 = dx * dx + dy * dy + dz * dz;
+    if (len2 < maxd2) {
+      int i = hn++;  // push into the max-heap
+      hd[i] = len2; hi[i] = ni;
+      while (i > 0) {
+        int par = (i - 1) >> 1;
+        if (hd[par] >= hd[i]) break;
+        double td = hd[par]; hd[par] = hd[i]; hd[i] = td;
+        int32_t ti = hi[par]; hi[par] = hi[i]; hi[i] = ti;
+        i = par;
+      }
+      if (hn > K) {  // poll the most distant
+        hn--;
+        hd[0] = hd[hn]; hi[0] = hi[hn];
+        int j = 0;
+        while (true) {
+          int l = 2 * j + 1, r = l + 1, m = j;
+          if (l < hn && hd[l] > hd[m]) m = l;
+          if (r < hn && hd[r] > hd[m]) m = r;
+          if (m == j) break;
+          double td = hd[m]; hd[m] = hd[j]; hd[j] = td;
+          int32_t ti = hi[m]; hi[m] = hi[j]; hi[j] = ti;
+          j = m;
+        }
+      }
+      if (hn == K && hd[0] < maxd2) maxd2 = hd[0];
+    }
+  }
+  if (hn == 0) return mk(0, 0, 0);  // [null] -> 0 (Q20)
+  double rSq = hd[0];
+  double area = PI_F * rSq;
+  V res = mk(0, 0, 0);
+  while (hn > 0) {  // sum in poll order (farthest first), as the reference's near_list
+    const PhotonD& ph = S.photon[hi[0]];
+    res.x += ph.pwr[0]; res.y += ph.pwr[1]; res.z += ph.pwr[2];
+    hn--;
+    hd[0] = hd[hn]; hi[0] = hi[hn];
+    int j = 0;
+    while (true) {
+      int l = 2 * j + 1, r = l + 1, m = j;
+      if (l < hn && hd[l] > hd[m]) m = l;
+      if (r < hn && hd[r] > hd[m]) m = r;
+      if (m == j) break;
+      double td = hd[m]; hd[m] = hd[j]; hd[j] = td;
+      int32_t ti = hi[m]; hi[m] = hi[j]; hi[j] = ti;
+      j = m;
+    }
+  }
+  return mk(res.x / area, res.y / area, res.z / area);
+}
+
+// skydome background (myScene.java:1104-1149)
+template <bool CNT, uint32_t F>
+DEVI V background(const SceneD& S, const WRay& w, Counters& ct) {
+  if constexpr ((F & FT_TEX) != 0) {
+    if (S.bkgTex >= 0) {
+      const TexD& T = S.tex[S.bkgTex];
+      double r = S.sky[0];
+      V c = mk(S.sky[1], S.sky[2], S.sky[3]);
+      V d = w.d, o = w.o;
+      double a = ((d.x / r) * (d.x / r)) + ((d.y / r) * (d.y / r)) + ((d.z / r) * (d.z / r));
+      V pC = mk((o.x - c.x) / r, (o.y - c.y) / r, (o.z - c.z) / r);
+      double b = 2 * (((d.x / r) * pC.x) + ((d.y / r) * pC.y) + ((d.z / r) * pC.z));
+      double cc = (pC.x * pC.x) + (pC.y * pC.y) + (pC.z * pC.z) - 1;
+      double discr = ((b * b) - (4 * a * cc));
+      double t = -DMAX;
+      if (discr > 0) {
+        double d1 = sqrt(discr), t1 = (-1 * b + d1) / (2 * a), t2 = (-1 * b - d1) / (2 * a), tv = jmin(t1, t2);
+        if (tv < EPS) tv = jmax(t1, t2);
+        t = tv;
+      }
+      V p = mk(d.x * t + o.x, d.y * t + o.y, d.z * t + o.z);
+      double a0 = p.y - c.y, a1 = a0 / r;
+      a1 = (a1 > 1) ? 1 : (a1 < -1) ? -1 : a1;
+      double v = (T.h - 1) * acos(a1) / PI_D;
+      double shWm1 = T.w - 1, z1 = (p.z - c.z), q = v / (T.h - 1);
+      double b0 = (p.x - c.x) / r;
+      b0 = (b0 > 1) ? 1 : (b0 < -1) ? -1 : b0;
+      double b1 = sin(q * PI_D);
+      double a2 = (fabs(b1) < EPS) ? 1 : b0 / b1;
+      double u = (z1 <= EPS) ? ((shWm1 * (acos(a2)) / (TWO_PI_F)) + shWm1 / 2.0) : shWm1 - ((shWm1 * (acos(a2)) / (TWO_PI_F)) + shWm1 / 2.0);
+      u = (u < 0) ? 0 : (u > shWm1) ? shWm1 : u;
+      if (CNT) ct.c[C_TEXEL]++;
+      return texel(S, T, (long)jd2i(v) * T.w + jd2i(u));
+    }
+  }
+  return mk(S.bg[0], S.bg[1], S.bg[2]);
+}
+
+DEVI V rot_axis(V v1, V u, double thet) {  // rotVecAroundAxis (DistRayTracer.java:336-349)
+  double cT = cos(thet), sT = sin(thet), oneMC = 1 - cT, ux2 = u.x * u.x, uy2 = u.y * u.y, uz2 = u.z * u.z,
+         uxy = u.x * u.y, uxz = u.x * u.z, uyz = u.y * u.z, uzS = u.z * sT, uyS = u.y * sT, uxS = u.x * sT,
+         uxzC1 = uxz * oneMC, uxyC1 = uxy * oneMC, uyzC1 = uyz * oneMC;
+  return mk((ux2 * oneMC + cT) * v1.x + (uxyC1 - uzS) * v1.y + (uxzC1 + uyS) * v1.z,
+            (uxyC1 + uzS) * v1.x + (uy2 * oneMC + cT) * v1.y + (uyzC1 - uxS) * v1.z,
+            (uxzC1 - uyS) * v1.x + (uyzC1 + uxS) * v1.y + (uz2 * oneMC + cT) * v1.z);
+}
+DEVI V disk_pos(const LightD& L, const Key& k, uint32_t kk) {  // getRandomDiskPos (myLight.java:251-258)
+  double th = rng(k.seed, k.pixel, k.sample, k.node, SITE_DISK + L.index, kk, 0, TWO_PI_F);
+  V r = nrmz(rot_axis(ld3(L.tangent), ld3(L.orient), th));
+  double m = rng(k.seed, k.pixel, k.sample, k.node, SITE_DISK + L.index, kk + 1, 0, L.radius);
+  r = mk(r.x * m, r.y * m, r.z * m);
+  return mk(r.x + L.origin[0], r.y + L.origin[1], r.z + L.origin[2]);
+}
+
+// calcShadowColor (myObjShader.java:98-153)
+template <bool CNT, uint32_t F>
+DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const Key& k, Counters& ct) {
+  double r = 0, g = 0, b = 0;
+  for (int li = 0; li < S.nlight; ++li) {
+    const LightD& L = S.light[li];
+    const bool disk = (F & FT_LIGHTX) && L.type == 2;
+    V lo = disk ? disk_pos(L, k, 0) : ld3(L.origin);
+    V ln = xpt(L.g, lo);
+    ln = nrmz(mk(ln.x - h.fwd.x, ln.y - h.fwd.y, ln.z - h.fwd.z));
+    WRay sr;
+    sr.o = h.fwd;
+    sr.d = nrmz(ln);  // myRay ctor normalises again
+    sr.d0 = sr.d;
+    sr.stable = false;
+    sr.moved = false;
+    sr.ver = 0;
+    V lo2 = disk ? disk_pos(L, k, 2) : ld3(L.origin);
+    double t = sqrt((((sr.o.x - lo2.x) * (sr.o.x - lo2.x)) + ((sr.o.y - lo2.y) * (sr.o.y - lo2.y))) + ((sr.o.z - lo2.z) * (sr.o.z - lo2.z)));
+    double ltMult = 1;
+    if (CNT) ct.c[C_LIGHT]++;
+    if ((F & FT_LIGHTX) && L.type == 1) {  // mySpotLight.intersectCheck / calcT_Mult (myLight.java:77-82,159-163)
+      double angle = acos(-1 * dot(sr.d, ld3(L.orient)));
+      ltMult = (angle < L.innerRad) ? 1 : (angle > L.outerRad) ? 0 : (L.outerRad - angle) / L.radDiff;
+    }
+    if (ltMult == 0) continue;
+    if (CNT) ct.c[C_SHADOW]++;
+    Key sk = k;
+    sk.tsite = SITE_SHADOW_TIME + li;
+    if (shadowed<CNT, F>(S, sr, sk, t, ct)) continue;
+    renorm(sr);  // shadowRay.direction._normalize()
+    double ldp = dot(sr.d, h.nrm) * ltMult;
+    if (ldp > EPS) {
+      r += tex.x * L.color[0] * ldp;
+      g += tex.y * L.color[1] * ldp;
+      b += tex.z * L.color[2] * ldp;
+    }
+    if (m.phong == 0) continue;
+    V hN = nrmz(mk(sr.d.x - h.dw.x, sr.d.y - h.dw.y, sr.d.z - h.dw.z));
+    double hdp = dot(hN, h.nrm) * ltMult;
+    if (hdp > EPS) {
+      double ph = pow(hdp * hdp, m.phong);
+      r += m.specular[0] * L.color[0] * ph;
+      g += m.specular[1] * L.color[1] * ph;
+      b += m.specular[2] * L.color[2] * ph;
+    }
+  }
+  return mk(r, g, b);
+}
+
+DEVI V refl_dir(V eye, V n) {  // compReflDir (myObjShader.java:89-96)
+  double dp = 2 * dot(eye, n);
+  V tv = mk(n.x * dp, n.y * dp, n.z * dp);
+  return nrmz(sub(tv, eye));
+}
+
+// Fresnel split shared by calcTransClr (myObjShader.java:157-276), calcTransRay
+// (:297-397, photons) and the simple shader's calcSimpleTransClr (:503-631).
+struct TransOut {
+  V refr, refl;  // refraction dir; reflection dir (already x refractNormMult)
+  double omtr, tr;
+  bool doA, doB;
+};
+DEVI TransOut trans_split(const MatD& m, const HitRec& h, const double* inKt, bool strans) {
+  TransOut T;
+  V back = mk(h.dw.x * -1, h.dw.y * -1, h.dw.z * -1);
+  V N = h.nrm;
+  double cos1 = dot(back, N), rnm = 1.0;
+  if (cos1 < EPS) { rnm = -1.0; N = mk(N.x * -1, N.y * -1, N.z * -1); }
+  cos1 = dot(back, N);
+  double mb = mag(back), mn = mag(N);
+  double thetaI = acos(dot(back, N) / (mb * mn));  // _angleBetween (DistRayTracer.java:445-452)
+  double idx = strans ? m.perm : m.ktrans;
+  double n = 1, n1 = 0, n2 = 0, cos2 = 0, tr = 0, omtr = 1;
+  bool TIR = false;
+  if (rnm < 0) {  // leaving the material
+    double thetaCrit = asin(1.0 / idx);
+    if (thetaI < thetaCrit) {
+      n1 = idx; n2 = 1; n = (n1 / n2);
+      cos2 = sqrt(1.0 - (n * n) * (1.0 - (cos1 * cos1)));
+    } else {
+      tr = 1; omtr = 1 - tr; TIR = true; cos2 = 0;
+    }
+  } else {
+    n1 = strans ? inKt[1] : inKt[0];
+    n2 = idx;
+    n = (n1 / n2);
+    cos2 = sqrt(1.0 - (n * n) * (1.0 - (cos1 * cos1)));
+  }
+  if (!TIR) {  // Fresnel with cos(theta_t) = sqrt(1 - (n1/n2) sin^2) (Q15)
+    double sa = sin(acos(cos1)), rct = sqrt(1.0 - ((n1 / n2) * sa * sa));
+    double a1 = n1 * cos1, b1 = n2 * rct, nd1 = (a1 - b1) / (a1 + b1);
+    double a2 = n1 * rct, b2 = n2 * cos1, nd2 = (a2 - b2) / (a2 + b2);
+    tr = ((nd1 * nd1) + (nd2 * nd2)) / 2.0;
+    omtr = 1 - tr;
+  }
+  T.omtr = omtr;
+  T.tr = tr;
+  T.doA = strans ? (omtr > 0) : (omtr > EPS);
+  T.doB = strans ? (tr > 0) : (tr > EPS);
+  V u = mk(back.x * (n * -1), back.y * (n * -1), back.z * (n * -1));
+  double kk = (n * cos1) - cos2;
+  V nv = mk(N.x * kk, N.y * kk, N.z * kk);
+  T.refr = nrmz(mk(u.x + nv.x, u.y + nv.y, u.z + nv.z));
+  V rd = refl_dir(back, N);
+  T.refl = mk(rd.x * rnm, rd.y * rnm, rd.z * rnm);
+  return T;
+}
+
+// ---------------------------------------------------------------------------
+// shading tree. A node spawns child A at once; a frame keeps what the node
+// needs when its children return: local colour, accumulated child sum,
+// weights, and (two-child nodes only) the second child's ray.
+struct Child {  // outgoing ray
+  V o, d;
+  double kt[5];
+  uint32_t node;
+  int32_t gen;
+};
+template <uint32_t F>
+struct FrameT {
+  V local, acc, wA, wB, org, dB;
+  double ktB[5];
+  uint32_t node;
+  int32_t gen;
+  uint8_t phase, hasB, kindB;  // kindB: counter class of child B
+};
+template <uint32_t F>
+struct FrameR {
+  V local, acc, wA;
+  uint8_t phase;
+};
+template <uint32_t F>
+using FrameOf = typename std::conditional<(F & FT_TRANS) != 0, FrameT<F>, FrameR<F>>::type;
+
+// getColorAtPos (myObjShader.java:409-438; simple shader :635-651): local colour and the
+// children. Returns the number of children (0..2); child A is written to `a`.
+template <bool CNT, uint32_t F>
+DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key& k, FrameOf<F>& Fr, Child& a,
+                    bool& branch, Counters& ct) {
+  const MatD& m = S.mat[h.mat];
+  double r = m.ambient[0], g = m.ambient[1], b = m.ambient[2];
+  if constexpr ((F & FT_PHOTON) != 0) {
+    if (!m.simple && (m.krefl == 0.0) && m.usePhotonMap) {
+      V ir = irradiance<CNT>(S, h.fwd, ct);
+      if (m.isCausticPhtn) { r += ir.x; g += ir.y; b += ir.z; }
+      else { r += m.diffuse[0] * ir.x; g += m.diffuse[1] * ir.y; b += m.diffuse[2] * ir.z; }
+    }
+  }
+  V tex = diff_color<CNT, F>(S, m, h, k, m.simple ? 1.0 : m.diffConst, ct);
+  V ls = light_sum<CNT, F>(S, m, h, tex, k, ct);
+  r += ls.x; g += ls.y; b += ls.z;
+  Fr.local = mk(r, g, b);
+  Fr.acc = mk(0, 0, 0);
+  branch = (in.gen < S.numRays - 2) && m.hasCaustic;
+  if (!branch) return 0;
+  a.o = h.fwd;
+  a.gen = in.gen + 1;
+  a.node = in.node * 2;
+  if constexpr ((F & FT_TRANS) != 0) {
+    bool trans = !m.simple && ((m.ktrans > 0) || (m.perm > 0.0));
+    bool strans = m.simple && (m.ktrans > 0);
+    if (trans || strans) {  // calcTransClr :157-276 / calcSimpleTransClr :503-631
+      TransOut T = trans_split(m, h, in.kt, strans);
+      double kt[5] = {m.ktrans, m.perm, m.permclr[0], m.permclr[1], m.permclr[2]};
+      Fr.hasB = 0;
+      Fr.org = h.fwd;
+      Fr.node = in.node;
+      Fr.gen = in.gen;
+      if (T.doB) {
+        Fr.dB = T.refl;
+        Fr.hasB = 1;
+        Fr.kindB = C_REFL;
+        for (int i = 0; i < 5; ++i) Fr.ktB[i] = strans ? 1.0 : kt[i];
+        if (strans) { double w = T.tr * m.krefl; Fr.wB = mk(w, w, w); }
+        else Fr.wB = mk((T.tr) * m.permclr[0], (T.tr) * m.permclr[1], (T.tr) * m.permclr[2]);
+      }
+      if (T.doA) {
+        a.d = T.refr;
+        for (int i = 0; i < 5; ++i) a.kt[i] = kt[i];
+        if (strans) { double w = T.omtr * m.ktrans; Fr.wA = mk(w, w, w); }
+        else Fr.wA = mk((T.omtr) * m.permclr[0], (T.omtr) * m.permclr[1], (T.omtr) * m.permclr[2]);
+        if (CNT) ct.c[C_REFR]++;
+        Fr.phase = 1;
+        return Fr.hasB ? 2 : 1;
+      }
+      if (Fr.hasB) {  // only the reflection child: spawn it as "B"
+        a.d = Fr.dB;
+        a.node = in.node * 2 + 1;
+        for (int i = 0; i < 5; ++i) a.kt[i] = Fr.ktB[i];
+        if (CNT) ct.c[C_REFL]++;
+        Fr.phase = 2;
+        Fr.hasB = 0;
+        return 1;
+      }
+      return 0;
+    }
+  }
+  if (m.krefl > 0.0) {  // calcReflClr :278-294
+    V back = mk(h.dw.x * -1, h.dw.y * -1, h.dw.z * -1);
+    V rd = refl_dir(back, h.nrm);
+    if (dot(rd, h.nrm) >= 0) {
+      a.d = rd;
+      for (int i = 0; i < 5; ++i) a.kt[i] = 1;
+      Fr.wA = mk(m.kreflclr[0], m.kreflclr[1], m.kreflclr[2]);
+      Fr.phase = 1;
+      if constexpr ((F & FT_TRANS) != 0) Fr.hasB = 0;
+      if (CNT) ct.c[C_REFL]++;
+      return 1;
+    }
+  }
+  return 0;
+}
+
+DEVI V clampc(V c) { return mk(jmin(1, c.x), jmin(1, c.y), jmin(1, c.z)); }  // myColor ctor
+
+static constexpr int MAX_FRAMES = 7;  // gen < numRays-2 = 6 -> at most 6 nodes with children
+
+// reflectRay (myScene.java:907-914) for the whole shading tree of one camera sample
+template <bool CNT, uint32_t F>
+DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
+  FrameOf<F> fr[MAX_FRAMES];
+  int sp = 0;
+  Child in;
+  in.o = org; in.d = dir; in.node = 1; in.gen = 0;
+  for (int i = 0; i < 5; ++i) in.kt[i] = 1;
+  while (true) {
+    V c;
+    {
+      WRay w;
+      w.o = in.o; w.d = nrmz(in.d); w.d0 = w.d; w.stable = false; w.moved = false; w.ver = 0;  // myRay ctor
+      k.node = in.node;
+      Best b = closest<CNT, F>(S, w, k, ct);
+      if (b.t == DMAX) {
+        c = background<CNT, F>(S, w, ct);
+      } else {
+        HitRec h = make_hit<F>(S, b, w, k);
+        bool branch;
+        Child a;
+        FrameOf<F>& Fr = fr[sp];
+        int nch = shade_node<CNT, F>(S, h, in, k, Fr, a, branch, ct);
+        if (nch > 0 && sp < MAX_FRAMES) {
+          sp++;
+          in = a;
+          continue;
+        }
+        c = branch ? clampc(add(Fr.local, Fr.acc)) : clampc(Fr.local);
+      }
+    }
+    // deliver finished colours upward
+    bool spawned = false;
+    while (sp > 0) {
+      FrameOf<F>& P = fr[sp - 1];
+      if (P.phase == 1) {
+        P.acc = mk(P.acc.x + (P.wA.x * c.x), P.acc.y + (P.wA.y * c.y), P.acc.z + (P.wA.z * c.z));
+        if constexpr ((F & FT_TRANS) != 0) {
+          if (P.hasB) {
+            P.phase = 2;
+            in.o = P.org; in.d = P.dB; in.gen = P.gen + 1; in.node = P.node * 2 + 1;
+            for (int i = 0; i < 5; ++i) in.kt[i] = P.ktB[i];
+            if (CNT) ct.c[C_REFL]++;
+            spawned = true;
+            break;
+          }
+        }
+      } else {
+        if constexpr ((F & FT_TRANS) != 0)
+          P.acc = mk(P.acc.x + (P.wB.x * c.x), P.acc.y + (P.wB.y * c.y), P.acc.z + (P.wB.z * c.z));
+      }
+      c = clampc(add(P.local, P.acc));
+      sp--;
+    }
+    if (!spawned) return c;
+  }
+}
+
+#ifndef RT_RENDER_WAVES
+#define RT_RENDER_WAVES 4
+#endif
+template <bool CNT, uint32_t F>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_RENDER_WAVES))) render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict__ argb,
+                                                    unsigned long long* __restrict__ gcount) {
+  // 8x8 pixel tile per wave
+  const int tilesX = (P.W + 7) >> 3;
+  const int tile = blockIdx.x;
+  const int tx = tile % tilesX, ty = tile / tilesX;
+  const int lane = threadIdx.x;
+  const int col = tx * 8 + (lane & 7);
+  const int ri = ty * 8 + (lane >> 3);  // row index within this render's rows
+  Counters ct;
+  if (CNT)
+    for (int i = 0; i < C_N; ++i) ct.c[i] = 0;
+  if (col < P.W && ri < P.nrows) {
+    const int row = P.row0 + ri * P.rowStep;
+    const double rayY = (-1 * (row - P.H / 2.0));
+    const double rayX = col - P.W / 2.0;
+    Key k;
+    k.seed = P.seed;
+    k.pixel = (uint64_t)row * (uint64_t)P.W + (uint64_t)col;
+    k.tsite = SITE_TIME;
+    V c;
+    const int n = P.spp;
+    if ((F & FT_DOF) && S.dof) {  // shootMultiDpthOfFldRays (myScene.java:1386-1406)
+      V lc = nrmz(mk(rayX, rayY, P.viewZ));
+      // ray(eye, lc) hits the focal plane z = -focal (myPlane, identity CTM): the ctor and
+      // getTransformedRay both normalise, then (o,1),(d,0) go through the identity inverse
+      const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+      V ld = nrmz(nrmz(lc));
+      V fo = xpt(I, mk(0, 0, 0)), fd = xvec(I, ld);
+      V fN = mk(0, 0, 1);
+      double pr = dot(fN, fd);
+      double t = -(dot(fN, fo) + S.lensFocal) / pr;
+      V fpt = mk(fd.x * t + fo.x, fd.y * t + fo.y, fd.z * t + fo.z);
+      double rs = 0, gs = 0, bs = 0;
+      for (int s = 0; s < n; ++s) {
+        double th = rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_DOF_ANG, 0, 0, TWO_PI_F);
+        V tt = nrmz(rot_axis(mk(0, 1, 0), mk(0, 0, -1), th));
+        double mm = rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_DOF_RAD, 0, 0, S.lensRadius);
+        tt = mk(tt.x * mm, tt.y * mm, tt.z * mm);
+        V o = mk(tt.x + lc.x, tt.y + lc.y, tt.z + lc.z);
+        k.sample = (uint32_t)s;
+        if (CNT) ct.c[C_CAMERA]++;
+        V cc = trace_sample<CNT, F>(S, o, sub(fpt, o), k, ct);
+        rs += cc.x; gs += cc.y; bs += cc.z;
+      }
+      c = clampc(mk(rs / n, gs / n, bs / n));
+    } else if (n == 1) {  // myFOVScene.draw 1-spp path (:1498-1508)
+      k.sample = 0;
+      if (CNT) ct.c[C_CAMERA]++;
+      c = trace_sample<CNT, F>(S, mk(0, 0, 0), mk(rayX, rayY, P.viewZ), k, ct);
+    } else {  // shootMultiRays (:1447-1462): y jitter drawn before x
+      double rs = 0, gs = 0, bs = 0;
+      for (int s = 0; s < n; ++s) {
+        double ry = rayY + rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_AA_Y, 0, -.5, .5);
+        double rx = rayX + rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_AA_X, 0, -.5, .5);
+        k.sample = (uint32_t)s;
+        if (CNT) ct.c[C_CAMERA]++;
+        V cc = trace_sample<CNT, F>(S, mk(0, 0, 0), mk(rx, ry, P.viewZ), k, ct);
+        rs += cc.x; gs += cc.y; bs += cc.z;
+      }
+      c = clampc(mk(rs / n, gs / n, bs / n));
+    }
+    const size_t o = (size_t)ri * P.W + col;
+    if (rgb) {
+      rgb[3 * o + 0] = (float)c.x;
+      rgb[3 * o + 1] = (float)c.y;
+      rgb[3 * o + 2] = (float)c.z;
+    }
+    if (argb) {  // myColor.getInt (myObjShader.java:671)
+      uint32_t v = (uint32_t)(255u << 24) + ((uint32_t)jd2i(c.x * 255) << 16) + ((uint32_t)jd2i(c.y * 255) << 8) +
+                   (uint32_t)jd2i(c.z * 255);
+      argb[o] = (int32_t)v;
+    }
+  }
+  if (CNT) {
+    for (int i = 0; i < C_N; ++i)
+      if (ct.c[i]) atomicAdd(&gcount[i], (unsigned long long)ct.c[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// photon pre-pass (myScene.sendCausticPhotons :952-998 / sendDiffusePhotons :1000-1091):
+// one lane per emitted photon (light-major, photon index minor). Each lane writes
+// its stored photons into PH_SLOTS slots in path order; the host compacts them in
+// (light, index, slot) order -- the reference's photon_list insertion order.
+static constexpr int PH_SLOTS = 6;
+static constexpr int PH_MAXTRY = 4096;  // rejection-sampling cap (reached with probability ~0)
+struct PhotonOut {
+  double pos[3];
+  double pwr[3];
+};
+// genRndPhtnRay (myLight.java:104-107 point, :165-185 spot, :229-242 disk; getRandDir :59-74)
+DEVI void photon_ray(const LightD& L, uint64_t seed, uint64_t i, V& o, V& d) {
+  uint32_t k = 0, li = (uint32_t)L.index;
+  if (L.type == 0) {
+    double x, y, z, sq;
+    int tries = 0;
+    do {
+      x = rng(seed, i, li, 0, SITE_PH_DIR, k++, -1.0, 1.0);
+      y = rng(seed, i, li, 0, SITE_PH_DIR, k++, -1.0, 1.0);
+      z = rng(seed, i, li, 0, SITE_PH_DIR, k++, -1.0, 1.0);
+      sq = (x * x) + (y * y) + (z * z);
+    } while (((sq > 1.0) || (sq < EPS)) && ++tries < PH_MAXTRY);
+    double m = sqrt(sq);
+    d = mk(x / m, y / m, z / m);
+    o = xpt(L.g, ld3(L.origin));
+    return;
+  }
+  if (L.type == 1) {
+    double checkProb = rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, 1), angle, prob;
+    int tries = 0;
+    do {
+      angle = rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, L.outerRad);
+      prob = (angle < L.innerRad) ? 1 : (angle > L.outerRad) ? 0 : (L.outerRad - angle) / L.radDiff;
+    } while (prob > checkProb && ++tries < PH_MAXTRY);
+    V t = nrmz(rot_axis(ld3(L.orient), ld3(L.tangent), angle));
+    d = rot_axis(t, ld3(L.orient), rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, TWO_PI_F));
+    o = xpt(L.g, ld3(L.origin));
+    return;
+  }
+  double angle, prob;
+  int tries = 0;
+  do {
+    angle = rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, PI_D);
+    prob = (angle < 0) ? 1 : (angle > PI_D) ? 0 : (PI_D - angle) / PI_D;
+  } while (prob > rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, 1) && ++tries < PH_MAXTRY);
+  V dd = nrmz(rot_axis(ld3(L.orient), ld3(L.tangent), angle));
+  d = rot_axis(dd, ld3(L.orient), rng(seed, i, li, 0, SITE_PH_DIR, k++, 0, TWO_PI_F));
+  Key kk;
+  kk.seed = seed; kk.pixel = i; kk.sample = li; kk.node = 0; kk.tsite = SITE_PH_TIME;
+  o = xpt(L.g, disk_pos(L, kk, 0));
+}
+// findCausticRayHit (myObjShader.java:461-478) with calcTransRay / calcReflRay
+DEVI bool caustic_ray(const SceneD& S, const HitRec& h, const double* inKt, int gen, double pwr[3], Child& out) {
+  const MatD& m = S.mat[h.mat];
+  if (!((gen < 4) && m.hasCaustic)) return false;  // numPhotonRays = 4
+  double pmul[3] = {1.0, 1.0, 1.0};
+  bool ok = false;
+  if ((m.ktrans > 0.0) || (m.perm > 0.0)) {
+    pmul[0] = m.phtnPermClr[0]; pmul[1] = m.phtnPermClr[1]; pmul[2] = m.phtnPermClr[2];
+    TransOut T = trans_split(m, h, inKt, false);
+    out.d = (T.omtr > EPS) ? T.refr : T.refl;
+    out.kt[0] = m.ktrans; out.kt[1] = m.perm; out.kt[2] = m.permclr[0]; out.kt[3] = m.permclr[1]; out.kt[4] = m.permclr[2];
+    ok = true;
+  } else if (m.krefl > 0.0) {
+    pmul[0] = pmul[1] = pmul[2] = m.krefl;
+    out.d = refl_dir(mk(h.dw.x * -1, h.dw.y * -1, h.dw.z * -1), h.nrm);
+    for (int c = 0; c < 5; ++c) out.kt[c] = 1;
+    ok = true;
+  }
+  for (int c = 0; c < 3; ++c) pwr[c] = pwr[c] * pmul[c];
+  out.o = h.fwd;
+  out.gen = gen + 1;
+  return ok;
+}
+DEVI void new_wray(WRay& w, V o, V d) {
+  w.o = o; w.d = nrmz(d); w.d0 = w.d; w.stable = false; w.moved = false; w.ver = 0;
+}
+
+__global__ void __launch_bounds__(64) photon_kernel(SceneD S, uint64_t seed, int numCast, int caustic, double pwrMult,
+                                                   PhotonOut* __restrict__ out, int* __restrict__ cnt) {
+  constexpr uint32_t F = FT_ALL;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)S.nlight * numCast) return;
+  const int li = (int)(gid / numCast);
+  const uint64_t i = (uint64_t)(gid % numCast);
+  const LightD& L = S.light[li];
+  Counters ct;
+  int n = 0;
+  PhotonOut* slot = out + gid * PH_SLOTS;
+  double pwr[3] = {L.color[0] * pwrMult, L.color[1] * pwrMult, L.color[2] * pwrMult};
+  Key k;
+  k.seed = seed; k.pixel = i; k.sample = (uint32_t)li; k.node = 0; k.tsite = SITE_PH_TIME;
+  WRay w;
+  V po, pd;
+  photon_ray(L, seed, i, po, pd);
+  new_wray(w, po, pd);
+  double kt[5] = {1, 1, 1, 1, 1};
+  int gen = 0;
+  Best b = closest<false, F>(S, w, k, ct);
+  if (b.t == DMAX) { cnt[gid] = 0; return; }
+  HitRec h = make_hit<F>(S, b, w, k);
+  if (caustic) {
+    if (!S.mat[h.mat].hasCaustic) { cnt[gid] = 0; return; }
+    int rgen = 0;
+    bool hit = true;
+    do {
+      Child c;
+      double cur[3] = {pwr[0], pwr[1], pwr[2]};
+      if (caustic_ray(S, h, kt, gen, cur, c)) {
+        for (int q = 0; q < 3; ++q) pwr[q] = cur[q];
+        for (int q = 0; q < 5; ++q) kt[q] = c.kt[q];
+        rgen = c.gen;
+        k.node = (uint32_t)rgen;
+        new_wray(w, c.o, c.d);
+        b = closest<false, F>(S, w, k, ct);
+        hit = b.t != DMAX;
+        if (hit) { h = make_hit<F>(S, b, w, k); gen = rgen; }
+      } else {
+        hit = false;
+      }
+    } while (hit && S.mat[h.mat].hasCaustic && rgen <= 4);
+    if (hit && rgen <= 4) {
+      for (int q = 0; q < 3; ++q) { slot[0].pos[q] = (&h.fwd.x)[q]; slot[0].pwr[q] = pwr[q]; }
+      n = 1;
+    }
+    cnt[gid] = n;
+    return;
+  }
+  bool done = false, firstDiff = true, hit = true;
+  uint32_t bounce = 0;
+  do {
+    bounce++;
+    const MatD& m = S.mat[h.mat];
+    if (m.krefl == 0) {
+      double prob = 0;
+      uint32_t kk = 0;
+      if (!firstDiff) {
+        if (n < PH_SLOTS) {
+          for (int q = 0; q < 3; ++q) { slot[n].pos[q] = (&h.fwd.x)[q]; slot[n].pwr[q] = pwr[q]; }
+          n++;
+        }
+        prob = rng(seed, i, (uint32_t)li, bounce, SITE_PH_BOUNCE, kk++, 0, 1.0);
+      }
+      firstDiff = false;
+      if (prob < m.avgDiffClr) {
+        double x = 0, y = 0, sq;
+        int tries = 0;
+        do {
+          x = rng(seed, i, (uint32_t)li, bounce, SITE_PH_BOUNCE, kk++, -1.0, 1.0);
+          y = rng(seed, i, (uint32_t)li, bounce, SITE_PH_BOUNCE, kk++, -1.0, 1.0);
+          sq = (x * x) + (y * y);
+        } while (((sq >= 1.0) || (sq < EPS)) && ++tries < PH_MAXTRY);
+        double z = sqrt(1 - (sq));
+        V nn = h.nrm;
+        double nx = nn.x * nn.x, ny = nn.y * nn.y, nz = nn.z * nn.z;
+        V tv = ((nx > ny) && (nx > nz)) ? mk(0, 0, 1) : mk(1, 0, 0);
+        V p_ = cross(nn, tv), q_ = cross(p_, nn);
+        nn = mk(nn.x * z, nn.y * z, nn.z * z);
+        p_ = mk(p_.x * x, p_.y * x, p_.z * x);
+        q_ = mk(q_.x * y, q_.y * y, q_.z * y);
+        V bd = nrmz(mk(nn.x + p_.x + q_.x, nn.y + p_.y + q_.y, nn.z + p_.z + q_.z));
+        for (int q = 0; q < 3; ++q) pwr[q] = pwr[q] * m.phtnDiffScl[q];
+        gen = gen + 1;
+        k.node = bounce;
+        new_wray(w, h.fwd, bd);
+        for (int q = 0; q < 5; ++q) kt[q] = 1;
+        b = closest<false, F>(S, w, k, ct);
+        hit = b.t != DMAX;
+        if (hit) h = make_hit<F>(S, b, w, k);
+      } else {
+        done = true;
+      }
+    } else {
+      Child c;
+      double cur[3] = {pwr[0], pwr[1], pwr[2]};
+      if (caustic_ray(S, h, kt, gen, cur, c)) {
+        for (int q = 0; q < 3; ++q) pwr[q] = cur[q];
+        for (int q = 0; q < 5; ++q) kt[q] = c.kt[q];
+        gen = c.gen;
+        k.node = bounce;
+        new_wray(w, c.o, c.d);
+        b = closest<false, F>(S, w, k, ct);
+        hit = b.t != DMAX;
+        if (hit) h = make_hit<F>(S, b, w, k);
+      } else {
+        hit = false;
+      }
+    }
+  } while (hit && !done && gen <= 4);
+  cnt[gid] = n;
+}
+
+}  // namespace dv
+}  // namespace rt

@@ -7,6 +7,7 @@ raise RTError.
 from __future__ import annotations
 
 import ctypes
+import os
 from pathlib import Path
 
 import numpy as np
@@ -43,7 +44,9 @@ _lib = None
 
 
 def lib_path() -> Path:
-    return _build.LIB_PATH
+    """The in-tree library; DISTRAYTRACER_LIB overrides it (tuning builds, tools/variant_sweep.py)."""
+    env = os.environ.get("DISTRAYTRACER_LIB")
+    return Path(env) if env else _build.LIB_PATH
 
 
 def lib():
@@ -106,9 +109,12 @@ def inspect_cli(cli: str, scene_dir=SCENE_DIR, textures: dict | None = None) -> 
     return dict(zip(INFO_NAMES, v.tolist()))
 
 
-def params(W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1) -> RenderParams:
+RENDER_GENERIC = 1  # RT_RENDER_GENERIC: the all-features kernel instead of the scene-specialised one
+
+
+def params(W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, flags=0) -> RenderParams:
     r0, r1 = (0, H) if rows is None else rows
-    return RenderParams(W, H, spp, r0, r1, row_step, seed, 0, 0)
+    return RenderParams(W, H, spp, r0, r1, row_step, seed, flags, 0)
 
 
 def nrows_of(p: RenderParams) -> int:
@@ -141,8 +147,8 @@ class Scene:
     def build_photons(self, seed: int):
         _check(lib().rt_photons_build(self._h, seed), "rt_photons_build")
 
-    def render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1):
-        p = params(W, H, spp, seed, rows, row_step)
+    def render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, flags=0):
+        p = params(W, H, spp, seed, rows, row_step, flags)
         n = nrows_of(p)
         rgb = np.zeros((n, W, 3), dtype=np.float32)
         argb = np.zeros((n, W), dtype=np.int32)
@@ -164,8 +170,8 @@ class Scene:
         _check(lib().rt_render_device(self._h, ctypes.byref(p), ctypes.c_void_p(rgb_ptr), ctypes.c_void_p(argb_ptr),
                                       ctypes.c_void_p(stream)), "rt_render_device")
 
-    def time_render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, warmup=1, iters=3) -> float:
-        p = params(W, H, spp, seed, rows, row_step)
+    def time_render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, warmup=1, iters=3, flags=0) -> float:
+        p = params(W, H, spp, seed, rows, row_step, flags)
         ms = ctypes.c_double(0)
         _check(lib().rt_time_render(self._h, ctypes.byref(p), warmup, iters, ctypes.byref(ms)), "rt_time_render")
         return ms.value

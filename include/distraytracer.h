@@ -138,9 +138,13 @@ typedef struct rt_render_params {
   int32_t row0, row1;    /* rows [row0,row1) of the image; row1 <= 0 means height */
   int32_t row_step;      /* <= 1: every row; >1: interleaved rows (multi-GPU bands) */
   uint64_t seed;         /* keyed RNG seed */
-  uint32_t flags;        /* reserved, 0 */
+  uint32_t flags;        /* RT_RENDER_* */
   int32_t pad;
 } rt_render_params;
+
+/* rt_render_params.flags: run the all-features kernel instead of the one specialised
+   to the scene's features (results are identical; for testing the specialisation) */
+#define RT_RENDER_GENERIC 1u
 
 typedef struct rt_scene rt_scene;
 

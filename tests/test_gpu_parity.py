@@ -113,3 +113,15 @@ def test_photon_map_parity(tmp_path, mode, spec):
     ro, ao, _ = o.render(64, 64, spp=2, seed=seed)
     c = compare(rg, ag, ro, ao)
     assert c["mismatch_frac"] < 5e-3, c
+
+
+@pytest.mark.parametrize("cli,W,spp", [("c3_bun69k.cli", 128, 2), ("t01.cli", 128, 1), ("p2_t05.cli", 96, 2),
+                                       ("c2clear.cli", 96, 1), ("plnts3ColsBunnies.cli", 96, 1)])
+def test_specialised_kernel_equals_generic(cli, W, spp):
+    """The feature-specialised kernel variant picked for a scene renders bit-identically
+    to the all-features kernel (RT_RENDER_GENERIC)."""
+    g = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+    rs, as_ = g.render(W, W, spp=spp, seed=SEED)
+    rg, ag = g.render(W, W, spp=spp, seed=SEED, flags=rt.RENDER_GENERIC)
+    assert np.array_equal(as_, ag)
+    assert np.array_equal(rs.view(np.uint32), rg.view(np.uint32))

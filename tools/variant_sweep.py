@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Kernel tuning sweep: build the library with different compile-time settings
+(here, on CPU) and time each on the GPU box, one subprocess per build.
+
+  python tools/variant_sweep.py build            # -> tools/_variants/*.so
+  python tools/variant_sweep.py run [--cfg C3]   # on the GPU: ms/frame + ARGB hash per build
+
+Every build must give the same ARGB hash (the specialisations change speed, not results).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+OUT = REPO / "tools" / "_variants"
+VARIANTS = {  # name -> -D defines
+    "w1": ["RT_RENDER_WAVES=1"],
+    "w2": ["RT_RENDER_WAVES=2"],
+    "w3": ["RT_RENDER_WAVES=3"],
+    "w4": ["RT_RENDER_WAVES=4"],
+    "w5": ["RT_RENDER_WAVES=5"],
+    "w6": ["RT_RENDER_WAVES=6"],
+    "w8": ["RT_RENDER_WAVES=8"],
+}
+
+
+def do_build(names):
+    from distraytracer_old_amd import build
+    for n in names:
+        p = build.build(defines=VARIANTS[n], out=OUT / f"lib_{n}.so")
+        print("built", p, flush=True)
+
+
+def time_one(cfg: str, W: int, H: int, spp: int, iters: int, flags: int):
+    from distraytracer_old_amd import rt, scenes
+    cli, W0, H0, spp0, seed = scenes.CONFIGS[cfg]
+    scenes.ensure_bun69k()
+    with rt.Scene.load_cli(cli, textures=scenes.prepare(cli)) as s:
+        W = W or W0; H = H or H0; spp = spp or spp0
+        _, argb = s.render(W, H, spp=spp, seed=seed, flags=flags)
+        ms = s.time_render(W, H, spp=spp, seed=seed, warmup=1, iters=iters, flags=flags)
+    return {"ms": ms, "hash": hashlib.sha1(argb.tobytes()).hexdigest()[:12], "W": W, "H": H, "spp": spp}
+
+
+def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["build", "run", "one"])
+    ap.add_argument("--cfg", default="C3")
+    ap.add_argument("--names", default=",".join(VARIANTS))
+    ap.add_argument("--W", type=int, default=0)
+    ap.add_argument("--H", type=int, default=0)
+    ap.add_argument("--spp", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--flags", type=int, default=0)
+    a = ap.parse_args()
+    names = a.names.split(",")
+    if a.mode == "build":
+        do_build(names)
+    elif a.mode == "one":
+        print(json.dumps(time_one(a.cfg, a.W, a.H, a.spp, a.iters, a.flags)))
+    else:
+        for n in names:
+            lib = OUT / f"lib_{n}.so"
+            env = dict(os.environ, DISTRAYTRACER_LIB=str(lib))
+            cmd = [sys.executable, __file__, "one", "--cfg", a.cfg, "--W", str(a.W), "--H", str(a.H), "--spp", str(a.spp),
+                   "--iters", str(a.iters), "--flags", str(a.flags)]
+            r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+            line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 and r.stdout.strip() else r.stderr[-800:]
+            print(n, a.cfg, line, flush=True)
+            if r.returncode != 0:
+                sys.exit(r.returncode)
+
+
+if __name__ == "__main__":
+    main()
