@@ -134,6 +134,9 @@ struct ParamsD {
   int32_t W, H, spp, row0, nrows, rowStep;
   uint64_t seed;
   double viewZ;
+  // wave layout: G lanes per pixel (power of two, G <= spp) trace samples j, j+G, ...;
+  // 64/G pixels per wave as a tw x th tile
+  int32_t G, tw, th, pad;
 };
 
 }  // namespace rt

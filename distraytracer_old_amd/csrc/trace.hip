@@ -165,6 +165,16 @@ static int make_params(rt_scene* s, const rt_render_params* p, ParamsD& P) {
   P.rowStep = step;
   P.nrows = (row1 - p->row0 + step - 1) / step;
   P.seed = p->seed;
+  // wave layout (render_kernel): G = largest power of two <= min(spp, 64) sample lanes per pixel
+  int G = 1;
+  while (G * 2 <= P.spp && G * 2 <= 64) G *= 2;
+  static const int TW[7] = {8, 8, 4, 4, 2, 2, 1};  // pixels per wave 64, 32, ..., 1 as tw x th
+  int lg = 0;
+  while ((1 << lg) < G) ++lg;
+  P.G = G;
+  P.tw = TW[lg];
+  P.th = (64 / G) / P.tw;
+  P.pad = 0;
   // myFOVScene.setSceneParams (myScene.java:1367-1381) at the requested resolution
   double fov = s->hs.fov, fovRad = M_PI * fov / 180.0;
   if (std::fabs(fov - 180) < .001) fovRad -= .0001;
@@ -216,7 +226,7 @@ static RenderFn pick_variant(const HostScene& h, uint32_t flags) {
 
 static int launch(rt_scene* s, const ParamsD& P, uint32_t flags, float* d_rgb, int32_t* d_argb, bool count,
                   hipStream_t st) {
-  int tilesX = (P.W + 7) / 8, tilesY = (P.nrows + 7) / 8;
+  int tilesX = (P.W + P.tw - 1) / P.tw, tilesY = (P.nrows + P.th - 1) / P.th;
   dim3 grid(tilesX * tilesY), block(64);
   if (count) {  // counting always runs the all-features kernel
     HIPCHK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long) * RT_ST_N, st));

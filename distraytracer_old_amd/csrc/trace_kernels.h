@@ -92,46 +92,41 @@ struct TFrame {
 template <bool CNT, uint32_t F>
 DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, Best& out, Counters& ct) {
   Best cur = miss();
-  if (A.root < 0) {
-    leaf_closest<CNT, F>(S, ~A.root, A.xf, ao, ad, w, k, cur, ct);
-  } else {
-    TFrame stk[BVH_STACK];
-    int sp = 0;
-    int32_t N = A.root;
-    while (true) {
-      // descend: push N, go left while the left box is hit
-      while (N >= 0) {
-        const NodeD& nd = S.node[N];
-        if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }  // both child boxes are tested once per visit
-        TFrame& f = stk[sp++];
-        f.nodePh = N << 1;
-        f.savedT = cur.t; f.savedRef = cur.ref; f.savedVer = cur.ver;
-        cur.t = DMAX;
-        double tL;
-        if (slab(nd.lmin, nd.lmax, ao, ad, tL)) N = nd.left;
-        else { N = INT32_MAX; break; }
-      }
-      if (N != INT32_MAX) leaf_closest<CNT, F>(S, ~N, A.xf, ao, ad, w, k, cur, ct);
-      // unwind
-      bool down = false;
-      while (sp > 0) {
-        TFrame& f = stk[sp - 1];
-        if ((f.nodePh & 1) == 0) {
-          const NodeD& nd = S.node[f.nodePh >> 1];
-          double tR;
-          if (slab(nd.rmin, nd.rmax, ao, ad, tR) && (cur.t == DMAX || tR < cur.t)) {
-            f.nodePh |= 1;
-            N = nd.right;
-            down = true;
-            break;
-          }
-        }
-        // node result = cur; merge into the enclosing context (saved wins ties: it is earlier)
-        if (f.savedT <= cur.t) { cur.t = f.savedT; cur.ref = f.savedRef; cur.ver = f.savedVer; }
-        sp--;
-      }
-      if (!down) break;
+  TFrame stk[BVH_STACK];
+  int sp = 0;
+  int32_t N = A.root;  // a leaf root (a plain list) is tested by the same loop with no frames
+  while (true) {
+    // descend: push N, go left while the left box is hit
+    while (N >= 0) {
+      const NodeD& nd = S.node[N];
+      if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }  // both child boxes are tested once per visit
+      TFrame& f = stk[sp++];
+      f.nodePh = N << 1;
+      f.savedT = cur.t; f.savedRef = cur.ref; f.savedVer = cur.ver;
+      cur.t = DMAX;
+      double tL;
+      if (slab(nd.lmin, nd.lmax, ao, ad, tL)) N = nd.left;
+      else { N = INT32_MAX; break; }
     }
+    if (N != INT32_MAX) leaf_closest<CNT, F>(S, ~N, A.xf, ao, ad, w, k, cur, ct);
+    // unwind
+    N = INT32_MAX;
+    while (sp > 0) {
+      TFrame& f = stk[sp - 1];
+      if ((f.nodePh & 1) == 0) {
+        const NodeD& nd = S.node[f.nodePh >> 1];
+        double tR;
+        if (slab(nd.rmin, nd.rmax, ao, ad, tR) && (cur.t == DMAX || tR < cur.t)) {
+          f.nodePh |= 1;
+          N = nd.right;
+          break;
+        }
+      }
+      // node result = cur; merge into the enclosing context (saved wins ties: it is earlier)
+      if (f.savedT <= cur.t) { cur.t = f.savedT; cur.ref = f.savedRef; cur.ver = f.savedVer; }
+      sp--;
+    }
+    if (N == INT32_MAX) break;
   }
   if (cur.t != DMAX) { cur.inAcc = 1; out = cur; }
   else out = miss();
@@ -195,39 +190,26 @@ DEVI bool leaf_any(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, co
 }
 template <bool CNT, uint32_t F>
 DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
-  if (A.root < 0) {  // leafVals.calcShadowHit: its own box first
-    if (!shadow_box<CNT>(A.bmin, A.bmax, ao, ad, dist, ct)) return false;
-    return leaf_any<CNT, F>(S, ~A.root, A.xf, ao, ad, w, k, dist, ct);
-  }
   int32_t stk[BVH_STACK];
   int sp = 0;
-  int32_t N = A.root;  // internal: no box test of its own (myBVH.calcShadowHit)
+  int32_t N = A.root;
+  // leafVals.calcShadowHit tests its own box first; myBVH.calcShadowHit (internal) does not
+  if (N < 0 && !shadow_box<CNT>(A.bmin, A.bmax, ao, ad, dist, ct)) return false;
   while (true) {
-    const NodeD& nd = S.node[N];
-    if (CNT) ct.c[C_NODE]++;
-    stk[sp++] = N;  // right child pending
-    bool down = false;
-    if (shadow_box<CNT>(nd.lmin, nd.lmax, ao, ad, dist, ct)) {
-      if (nd.left < 0) {
-        if (leaf_any<CNT, F>(S, ~nd.left, A.xf, ao, ad, w, k, dist, ct)) return true;
-      } else {
-        N = nd.left;
-        down = true;
-      }
+    if (N >= 0) {  // internal: push (right child pending), go left if its box is hit
+      const NodeD& nd = S.node[N];
+      if (CNT) ct.c[C_NODE]++;
+      stk[sp++] = N;
+      if (shadow_box<CNT>(nd.lmin, nd.lmax, ao, ad, dist, ct)) { N = nd.left; continue; }
+    } else if (N != INT32_MAX) {
+      if (leaf_any<CNT, F>(S, ~N, A.xf, ao, ad, w, k, dist, ct)) return true;
     }
-    if (down) continue;
-    while (true) {
-      if (sp == 0) return false;
+    N = INT32_MAX;
+    while (sp > 0) {
       const NodeD& pn = S.node[stk[--sp]];
-      if (shadow_box<CNT>(pn.rmin, pn.rmax, ao, ad, dist, ct)) {
-        if (pn.right < 0) {
-          if (leaf_any<CNT, F>(S, ~pn.right, A.xf, ao, ad, w, k, dist, ct)) return true;
-          continue;
-        }
-        N = pn.right;
-        break;
-      }
+      if (shadow_box<CNT>(pn.rmin, pn.rmax, ao, ad, dist, ct)) { N = pn.right; break; }
     }
+    if (N == INT32_MAX) return false;
   }
 }
 // myScene.calcShadow (myScene.java:879-885)
@@ -880,71 +862,98 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
 }
 
 #ifndef RT_RENDER_WAVES
-#define RT_RENDER_WAVES 4
+#define RT_RENDER_WAVES 5
 #endif
 template <bool CNT, uint32_t F>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_RENDER_WAVES))) render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict__ argb,
-                                                    unsigned long long* __restrict__ gcount) {
-  // 8x8 pixel tile per wave
-  const int tilesX = (P.W + 7) >> 3;
-  const int tile = blockIdx.x;
-  const int tx = tile % tilesX, ty = tile / tilesX;
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_RENDER_WAVES)))
+render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict__ argb, unsigned long long* __restrict__ gcount) {
+  // One wave = a tw x th pixel tile x G sample lanes per pixel. Samples of one pixel are
+  // nearly the same ray, so the G lanes of a pixel traverse the same nodes (coherent
+  // loads, little divergence). Lane j of a pixel traces samples j, j+G, ...; each round's
+  // G colours go through LDS and the pixel's first lane adds them in sample order, so
+  // the per-pixel sum is the reference's sequential sum (myScene.java:1451-1460).
+  __shared__ double cbuf[64 * 3];
   const int lane = threadIdx.x;
-  const int col = tx * 8 + (lane & 7);
-  const int ri = ty * 8 + (lane >> 3);  // row index within this render's rows
+  const int G = P.G;
+  const int j = lane & (G - 1), pl = lane / G;
+  const int tilesX = (P.W + P.tw - 1) / P.tw;
+  const int tx = blockIdx.x % tilesX, ty = blockIdx.x / tilesX;
+  const int col = tx * P.tw + pl % P.tw;
+  const int ri = ty * P.th + pl / P.tw;  // row index within this render's rows
+  const bool valid = col < P.W && ri < P.nrows;
   Counters ct;
   if (CNT)
     for (int i = 0; i < C_N; ++i) ct.c[i] = 0;
-  if (col < P.W && ri < P.nrows) {
-    const int row = P.row0 + ri * P.rowStep;
-    const double rayY = (-1 * (row - P.H / 2.0));
-    const double rayX = col - P.W / 2.0;
-    Key k;
-    k.seed = P.seed;
-    k.pixel = (uint64_t)row * (uint64_t)P.W + (uint64_t)col;
-    k.tsite = SITE_TIME;
-    V c;
-    const int n = P.spp;
-    if ((F & FT_DOF) && S.dof) {  // shootMultiDpthOfFldRays (myScene.java:1386-1406)
-      V lc = nrmz(mk(rayX, rayY, P.viewZ));
-      // ray(eye, lc) hits the focal plane z = -focal (myPlane, identity CTM): the ctor and
-      // getTransformedRay both normalise, then (o,1),(d,0) go through the identity inverse
-      const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-      V ld = nrmz(nrmz(lc));
-      V fo = xpt(I, mk(0, 0, 0)), fd = xvec(I, ld);
-      V fN = mk(0, 0, 1);
-      double pr = dot(fN, fd);
-      double t = -(dot(fN, fo) + S.lensFocal) / pr;
-      V fpt = mk(fd.x * t + fo.x, fd.y * t + fo.y, fd.z * t + fo.z);
-      double rs = 0, gs = 0, bs = 0;
-      for (int s = 0; s < n; ++s) {
+  const int row = P.row0 + ri * P.rowStep;
+  const double rayY = (-1 * (row - P.H / 2.0));
+  const double rayX = col - P.W / 2.0;
+  Key k;
+  k.seed = P.seed;
+  k.pixel = (uint64_t)row * (uint64_t)P.W + (uint64_t)col;
+  k.tsite = SITE_TIME;
+  const int n = P.spp;
+  const bool dof = (F & FT_DOF) && S.dof;
+  V fpt = mk(0, 0, 0), lc = mk(0, 0, 0);
+  if (dof && valid) {  // shootMultiDpthOfFldRays (myScene.java:1386-1406)
+    lc = nrmz(mk(rayX, rayY, P.viewZ));
+    // ray(eye, lc) hits the focal plane z = -focal (myPlane, identity CTM): the ctor and
+    // getTransformedRay both normalise, then (o,1),(d,0) go through the identity inverse
+    const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    V ld = nrmz(nrmz(lc));
+    V fo = xpt(I, mk(0, 0, 0)), fd = xvec(I, ld);
+    V fN = mk(0, 0, 1);
+    double pr = dot(fN, fd);
+    double t = -(dot(fN, fo) + S.lensFocal) / pr;
+    fpt = mk(fd.x * t + fo.x, fd.y * t + fo.y, fd.z * t + fo.z);
+  }
+  double rs = 0, gs = 0, bs = 0;
+  V c1 = mk(0, 0, 0);
+  for (int s0 = 0; s0 < n; s0 += G) {
+    const int s = s0 + j;
+    V cc = mk(0, 0, 0);
+    if (valid && s < n) {
+      V o, d;
+      if (dof) {
         double th = rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_DOF_ANG, 0, 0, TWO_PI_F);
         V tt = nrmz(rot_axis(mk(0, 1, 0), mk(0, 0, -1), th));
         double mm = rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_DOF_RAD, 0, 0, S.lensRadius);
         tt = mk(tt.x * mm, tt.y * mm, tt.z * mm);
-        V o = mk(tt.x + lc.x, tt.y + lc.y, tt.z + lc.z);
-        k.sample = (uint32_t)s;
-        if (CNT) ct.c[C_CAMERA]++;
-        V cc = trace_sample<CNT, F>(S, o, sub(fpt, o), k, ct);
-        rs += cc.x; gs += cc.y; bs += cc.z;
-      }
-      c = clampc(mk(rs / n, gs / n, bs / n));
-    } else if (n == 1) {  // myFOVScene.draw 1-spp path (:1498-1508)
-      k.sample = 0;
-      if (CNT) ct.c[C_CAMERA]++;
-      c = trace_sample<CNT, F>(S, mk(0, 0, 0), mk(rayX, rayY, P.viewZ), k, ct);
-    } else {  // shootMultiRays (:1447-1462): y jitter drawn before x
-      double rs = 0, gs = 0, bs = 0;
-      for (int s = 0; s < n; ++s) {
+        o = mk(tt.x + lc.x, tt.y + lc.y, tt.z + lc.z);
+        d = sub(fpt, o);
+      } else if (n == 1) {  // myFOVScene.draw 1-spp path (:1498-1508): no jitter, no averaging
+        o = mk(0, 0, 0);
+        d = mk(rayX, rayY, P.viewZ);
+      } else {  // shootMultiRays (:1447-1462): y jitter drawn before x
         double ry = rayY + rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_AA_Y, 0, -.5, .5);
         double rx = rayX + rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_AA_X, 0, -.5, .5);
-        k.sample = (uint32_t)s;
-        if (CNT) ct.c[C_CAMERA]++;
-        V cc = trace_sample<CNT, F>(S, mk(0, 0, 0), mk(rx, ry, P.viewZ), k, ct);
-        rs += cc.x; gs += cc.y; bs += cc.z;
+        o = mk(0, 0, 0);
+        d = mk(rx, ry, P.viewZ);
       }
-      c = clampc(mk(rs / n, gs / n, bs / n));
+      Key ks = k;
+      ks.sample = (uint32_t)s;
+      if (CNT) ct.c[C_CAMERA]++;
+      cc = trace_sample<CNT, F>(S, o, d, ks, ct);
     }
+    if (G == 1) {
+      c1 = cc;
+      rs += cc.x; gs += cc.y; bs += cc.z;
+    } else {
+      cbuf[3 * lane + 0] = cc.x;
+      cbuf[3 * lane + 1] = cc.y;
+      cbuf[3 * lane + 2] = cc.z;
+      __syncthreads();
+      if (j == 0) {
+        const int m = (n - s0) < G ? (n - s0) : G;
+        for (int q = 0; q < m; ++q) {
+          const double* b = cbuf + 3 * (pl * G + q);
+          rs += b[0]; gs += b[1]; bs += b[2];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (valid && j == 0) {
+    V c = (n == 1 && !dof) ? c1 : clampc(mk(rs / n, gs / n, bs / n));
     const size_t o = (size_t)ri * P.W + col;
     if (rgb) {
       rgb[3 * o + 0] = (float)c.x;
