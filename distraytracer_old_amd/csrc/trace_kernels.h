@@ -56,9 +56,16 @@ DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, double&
 template <uint32_t F>
 DEVI int32_t ref_xf(const SceneD& S, int32_t ref) { return (!(F & FT_PRIM) || ref >= 0) ? S.tri[ref].xf : S.prim[~ref].xf; }
 
+// The reference returns a best hit per BVH node and merges children keeping the first of
+// equal t (TreeMap); over the whole scan that is "the first-visited hit of minimal t", so
+// one running best with strict-< replacement in visit order gives the same answer. What
+// the per-node results are still needed for is the pruning rule (below), which only
+// needs each subtree's minimal t -- a double per stack frame.
+
 // myGeomList.traverseStruct leaf loop (myGeomBase.java:281-296): strict <, leaf order
 template <bool CNT, uint32_t F>
-DEVI void leaf_closest(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, const Key& k, Best& cur, Counters& ct) {
+DEVI void leaf_closest(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, const Key& k, int top, Best& best,
+                       double& local, Counters& ct) {
   LeafD lf = S.leaf[leaf];
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
   for (int i = 0; i < lf.count; ++i) {
@@ -70,8 +77,9 @@ DEVI void leaf_closest(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w
     else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
     double t;
     int args;
-    if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct) && t < cur.t) {
-      cur.t = t; cur.ref = ref; cur.ver = w.ver;
+    if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct)) {
+      if (t < local) local = t;
+      if (t < best.t) { best.t = t; best.ref = ref; best.ver = w.ver; best.top = (int16_t)top; best.inAcc = 1; }
     }
   }
 }
@@ -80,56 +88,51 @@ static constexpr int BVH_STACK = 40;  // host rejects BVHs deeper than 40
 
 // myAccelStruct.intersectCheck + myBVH.traverseStruct (myGeomBase.java:216-222, 407-421),
 // iteratively with the reference's LOCAL pruning: the right child is visited iff its
-// box is hit and (left subtree missed or box entry t < the LEFT SUBTREE's best t);
-// ties go left. Each pushed frame saves the enclosing context's best; the right box is
-// tested when the left subtree is done, as the Java does.
-struct TFrame {
-  double savedT;
-  int32_t nodePh;  // node << 1 | phase (0: left subtree in progress, 1: right)
-  int32_t savedRef;
-  uint32_t savedVer;
-};
+// box is hit and (left subtree missed or box entry t < the LEFT SUBTREE's minimal t);
+// ties go left. A frame = the enclosing subtree's minimal t so far + node<<1|phase; the
+// right box is tested when the left subtree is done, as the Java does.
 template <bool CNT, uint32_t F>
-DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, Best& out, Counters& ct) {
-  Best cur = miss();
-  TFrame stk[BVH_STACK];
+DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, int top, Best& best,
+                        Counters& ct) {
+  double stT[BVH_STACK];
+  int32_t stN[BVH_STACK];
   int sp = 0;
+  double local = DMAX;
   int32_t N = A.root;  // a leaf root (a plain list) is tested by the same loop with no frames
   while (true) {
     // descend: push N, go left while the left box is hit
     while (N >= 0) {
       const NodeD& nd = S.node[N];
       if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }  // both child boxes are tested once per visit
-      TFrame& f = stk[sp++];
-      f.nodePh = N << 1;
-      f.savedT = cur.t; f.savedRef = cur.ref; f.savedVer = cur.ver;
-      cur.t = DMAX;
+      stT[sp] = local;
+      stN[sp] = N << 1;
+      sp++;
+      local = DMAX;
       double tL;
       if (slab(nd.lmin, nd.lmax, ao, ad, tL)) N = nd.left;
       else { N = INT32_MAX; break; }
     }
-    if (N != INT32_MAX) leaf_closest<CNT, F>(S, ~N, A.xf, ao, ad, w, k, cur, ct);
+    if (N != INT32_MAX) leaf_closest<CNT, F>(S, ~N, A.xf, ao, ad, w, k, top, best, local, ct);
     // unwind
     N = INT32_MAX;
     while (sp > 0) {
-      TFrame& f = stk[sp - 1];
-      if ((f.nodePh & 1) == 0) {
-        const NodeD& nd = S.node[f.nodePh >> 1];
+      const int32_t np = stN[sp - 1];
+      if ((np & 1) == 0) {
+        const NodeD& nd = S.node[np >> 1];
         double tR;
-        if (slab(nd.rmin, nd.rmax, ao, ad, tR) && (cur.t == DMAX || tR < cur.t)) {
-          f.nodePh |= 1;
+        if (slab(nd.rmin, nd.rmax, ao, ad, tR) && (local == DMAX || tR < local)) {
+          stN[sp - 1] = np | 1;
           N = nd.right;
           break;
         }
       }
-      // node result = cur; merge into the enclosing context (saved wins ties: it is earlier)
-      if (f.savedT <= cur.t) { cur.t = f.savedT; cur.ref = f.savedRef; cur.ver = f.savedVer; }
+      // this node's minimal t joins the enclosing subtree's
+      const double sv = stT[sp - 1];
+      if (sv < local) local = sv;
       sp--;
     }
     if (N == INT32_MAX) break;
   }
-  if (cur.t != DMAX) { cur.inAcc = 1; out = cur; }
-  else out = miss();
 }
 
 // findClosestRayHit (myScene.java:888-903): objList scan, TreeMap keeps the first of equal t
@@ -148,9 +151,7 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       double te;
       if (!slab(A.bmin, A.bmax, o, d, te)) continue;
       w.moved = false;
-      Best r;
-      accel_closest<CNT, F>(S, A, o, d, w, k, r, ct);
-      if (r.t < best.t) { best = r; best.top = (int16_t)i; }
+      accel_closest<CNT, F>(S, A, o, d, w, k, i, best, ct);
     } else {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
@@ -713,8 +714,9 @@ struct FrameT {
   uint8_t phase, hasB, kindB;  // kindB: counter class of child B
 };
 template <uint32_t F>
-struct FrameR {
-  V local, acc, wA;
+struct FrameR {  // no transparent materials: at most one child (reflection), weight = mat.kreflclr
+  V local;
+  int32_t mat;
   uint8_t phase;
 };
 template <uint32_t F>
@@ -738,7 +740,7 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
   V ls = light_sum<CNT, F>(S, m, h, tex, k, ct);
   r += ls.x; g += ls.y; b += ls.z;
   Fr.local = mk(r, g, b);
-  Fr.acc = mk(0, 0, 0);
+  if constexpr ((F & FT_TRANS) != 0) Fr.acc = mk(0, 0, 0);
   branch = (in.gen < S.numRays - 2) && m.hasCaustic;
   if (!branch) return 0;
   a.o = h.fwd;
@@ -789,9 +791,13 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
     if (dot(rd, h.nrm) >= 0) {
       a.d = rd;
       for (int i = 0; i < 5; ++i) a.kt[i] = 1;
-      Fr.wA = mk(m.kreflclr[0], m.kreflclr[1], m.kreflclr[2]);
       Fr.phase = 1;
-      if constexpr ((F & FT_TRANS) != 0) Fr.hasB = 0;
+      if constexpr ((F & FT_TRANS) != 0) {
+        Fr.wA = mk(m.kreflclr[0], m.kreflclr[1], m.kreflclr[2]);
+        Fr.hasB = 0;
+      } else {
+        Fr.mat = h.mat;
+      }
       if (CNT) ct.c[C_REFL]++;
       return 1;
     }
@@ -831,17 +837,22 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
           in = a;
           continue;
         }
-        c = branch ? clampc(add(Fr.local, Fr.acc)) : clampc(Fr.local);
+        c = branch ? clampc(add(Fr.local, mk(0, 0, 0))) : clampc(Fr.local);  // no child: acc stayed 0
       }
     }
     // deliver finished colours upward
     bool spawned = false;
     while (sp > 0) {
       FrameOf<F>& P = fr[sp - 1];
-      if (P.phase == 1) {
-        P.acc = mk(P.acc.x + (P.wA.x * c.x), P.acc.y + (P.wA.y * c.y), P.acc.z + (P.wA.z * c.z));
-        if constexpr ((F & FT_TRANS) != 0) {
-          if (P.hasB) {
+      if constexpr ((F & FT_TRANS) == 0) {  // the only child has returned
+        const double* wA = S.mat[P.mat].kreflclr;
+        V acc = mk(0 + (wA[0] * c.x), 0 + (wA[1] * c.y), 0 + (wA[2] * c.z));
+        c = clampc(add(P.local, acc));
+        sp--;
+      } else {
+        if (P.phase == 1) {
+          P.acc = mk(P.acc.x + (P.wA.x * c.x), P.acc.y + (P.wA.y * c.y), P.acc.z + (P.wA.z * c.z));
+          if (P.hasB) {  // second child (Fresnel reflection)
             P.phase = 2;
             in.o = P.org; in.d = P.dB; in.gen = P.gen + 1; in.node = P.node * 2 + 1;
             for (int i = 0; i < 5; ++i) in.kt[i] = P.ktB[i];
@@ -849,13 +860,12 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
             spawned = true;
             break;
           }
-        }
-      } else {
-        if constexpr ((F & FT_TRANS) != 0)
+        } else {
           P.acc = mk(P.acc.x + (P.wB.x * c.x), P.acc.y + (P.wB.y * c.y), P.acc.z + (P.wB.z * c.z));
+        }
+        c = clampc(add(P.local, P.acc));
+        sp--;
       }
-      c = clampc(add(P.local, P.acc));
-      sp--;
     }
     if (!spawned) return c;
   }
