@@ -128,6 +128,7 @@ struct SceneD {
   int32_t dof;
   double lensRadius, lensFocal;
   int32_t numRays;  // recursion budget (myScene.numRays = 8)
+  int32_t fastSlab; // every BVH box coordinate is 0 or in [2^-200, 2^200] (trace_device.h qdiv)
 };
 
 struct ParamsD {

@@ -74,6 +74,18 @@ static int upload_scene(rt_scene* s) {
   d.lensRadius = h.lensRadius;
   d.lensFocal = h.lensFocal;
   d.numRays = 8;  // myScene.numRays
+  // qdiv (trace_device.h) is exact only for box coordinates 0 or in [2^-200, 2^200]
+  auto in_range = [](const double* c, int n) {
+    for (int i = 0; i < n; ++i) {
+      double a = std::fabs(c[i]);
+      if (!(c[i] == 0 || (a >= 0x1p-200 && a <= 0x1p200))) return false;
+    }
+    return true;
+  };
+  bool ok = true;
+  for (const NodeD& n : h.node) ok = ok && in_range(n.lmin, 3) && in_range(n.lmax, 3) && in_range(n.rmin, 3) && in_range(n.rmax, 3);
+  for (const AccelD& a : h.accel) ok = ok && in_range(a.bmin, 3) && in_range(a.bmax, 3);
+  d.fastSlab = ok ? 1 : 0;
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dv::c_perm), H_PERM, sizeof(H_PERM)));
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dv::c_grad3), H_GRAD3, sizeof(H_GRAD3)));
   void* cnt = nullptr;
@@ -230,10 +242,10 @@ static int launch(rt_scene* s, const ParamsD& P, uint32_t flags, float* d_rgb, i
   dim3 grid(tilesX * tilesY), block(64);
   if (count) {  // counting always runs the all-features kernel
     HIPCHK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long) * RT_ST_N, st));
-    hipLaunchKernelGGL((dv::render_kernel<true, dv::FT_ALL>), grid, block, 0, st, s->dev, P, d_rgb, d_argb,
+    hipLaunchKernelGGL((dv::render_kernel<true, dv::FT_ALL>), grid, block, dv::LDS_BYTES, st, s->dev, P, d_rgb, d_argb,
                        (unsigned long long*)s->counters);
   } else {
-    hipLaunchKernelGGL(pick_variant(s->hs, flags), grid, block, 0, st, s->dev, P, d_rgb, d_argb,
+    hipLaunchKernelGGL(pick_variant(s->hs, flags), grid, block, dv::LDS_BYTES, st, s->dev, P, d_rgb, d_argb,
                        (unsigned long long*)nullptr);
   }
   HIPCHK(hipGetLastError());
@@ -336,7 +348,7 @@ extern "C" int rt_photons_build(rt_scene* s, uint64_t seed) {
     bool caustic = h.photonMode == 2;
     double pwrMult = (caustic ? 40.0 : 8.0) / h.photonCount;  // causticsLightPwrMult / diffuseLightPwrMult (myScene.java:109-110)
     long blocks = (total + 63) / 64;
-    hipLaunchKernelGGL(dv::photon_kernel, dim3((unsigned)blocks), dim3(64), 0, 0, s->dev, seed, h.photonCount, caustic ? 1 : 0,
+    hipLaunchKernelGGL(dv::photon_kernel, dim3((unsigned)blocks), dim3(64), dv::LDS_BYTES, 0, s->dev, seed, h.photonCount, caustic ? 1 : 0,
                        pwrMult, d_out, d_cnt);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipDeviceSynchronize();

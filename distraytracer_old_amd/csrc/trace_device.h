@@ -10,6 +10,8 @@
 #include <stdint.h>
 
 #include "rt_types.h"
+#define QD_FN __device__ __forceinline__
+#include "qdiv.h"
 
 namespace rt {
 namespace dv {
@@ -132,14 +134,26 @@ struct Counters {
 // ---------------------------------------------------------------------------
 // primitive tests (object space). `args` carries what the hit record needs:
 // planar orientation, cylinder face, box plane.
-DEVI bool slab(const double* mn, const double* mx, V o, V d, double& tEntry) {  // myBBox.intersectCheck :132-162
+struct RayInv {
+  double y[3];  // RN(1 / d_i)
+  bool fast;    // qdiv is exact for this ray (see qdiv)
+};
+DEVI RayInv ray_inv(V o, V d, int sceneOk) {
+  RayInv r;
+  r.y[0] = 1.0 / d.x; r.y[1] = 1.0 / d.y; r.y[2] = 1.0 / d.z;
+  r.fast = sceneOk && qd_range(d.x) && qd_range(d.y) && qd_range(d.z) && qc_range(o.x) && qc_range(o.y) && qc_range(o.z);
+  return r;
+}
+
+template <bool FAST>
+DEVI bool slab_t(const double* mn, const double* mx, V o, V d, const double* y, double& tEntry) {  // myBBox.intersectCheck :132-162
   double ro[3] = {o.x, o.y, o.z}, rd[3] = {d.x, d.y, d.z};
   double tMin[3], tMax[3];
   double biggestMin = -DMAX;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    double t1 = (mn[i] - ro[i]) / rd[i];
-    double t2 = (mx[i] - ro[i]) / rd[i];
+    double t1 = FAST ? qdiv(mn[i] - ro[i], rd[i], y[i]) : (mn[i] - ro[i]) / rd[i];
+    double t2 = FAST ? qdiv(mx[i] - ro[i], rd[i], y[i]) : (mx[i] - ro[i]) / rd[i];
     if (t1 < t2) {
       tMin[i] = t1; tMax[i] = t2;
       if (biggestMin < t1) biggestMin = t1;
@@ -156,6 +170,13 @@ DEVI bool slab(const double* mn, const double* mx, V o, V d, double& tEntry) {  
   }
   tEntry = biggestMin;
   return (mnv > mxv) && biggestMin > 0;
+}
+DEVI bool slab(const double* mn, const double* mx, V o, V d, double& tEntry) {
+  return slab_t<false>(mn, mx, o, d, nullptr, tEntry);
+}
+DEVI bool slab(const double* mn, const double* mx, V o, V d, const RayInv& ri, double& tEntry) {
+  if (ri.fast) return slab_t<true>(mn, mx, o, d, ri.y, tEntry);
+  return slab_t<false>(mn, mx, o, d, nullptr, tEntry);
 }
 DEVI int slab_plane(const double* mn, const double* mx, V o, V d) {  // plane idx for myBBox normals
   double ro[3] = {o.x, o.y, o.z}, rd[3] = {d.x, d.y, d.z};

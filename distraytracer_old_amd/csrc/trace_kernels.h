@@ -86,16 +86,63 @@ DEVI void leaf_closest(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w
 
 static constexpr int BVH_STACK = 40;  // host rejects BVHs deeper than 40
 
+// Traversal stacks: the first STK_LDS levels live in LDS ([level][lane], conflict-free),
+// deeper levels in scratch. The closest-hit and shadow traversals never overlap in time,
+// so they share the LDS node-index array. One wave per workgroup.
+#ifndef RT_STACK_LDS
+#define RT_STACK_LDS 12
+#endif
+static constexpr int STK_LDS = RT_STACK_LDS;
+// dynamic LDS of every kernel here: the traversal stack, aliased by render_kernel's
+// per-round sample colours (used only between traversals)
+extern __shared__ double rt_lds[];
+static constexpr int LDS_STACK_BYTES = STK_LDS * 64 * 12;
+static constexpr int LDS_BYTES = LDS_STACK_BYTES > 64 * 3 * 8 ? LDS_STACK_BYTES : 64 * 3 * 8;
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+DEVI lds_f64* ldsT() { return (lds_f64*)rt_lds; }
+DEVI lds_i32* ldsN() { return (lds_i32*)(rt_lds + STK_LDS * 64); }
+struct Stack {
+  double sT[BVH_STACK - STK_LDS];
+  int32_t sN[BVH_STACK - STK_LDS];
+  DEVI double getT(int i) const {
+    if (i < STK_LDS) return ldsT()[i * 64 + threadIdx.x];
+    return sT[i - STK_LDS];
+  }
+  DEVI void setT(int i, double v) {
+    if (i < STK_LDS) ldsT()[i * 64 + threadIdx.x] = v;
+    else sT[i - STK_LDS] = v;
+  }
+  DEVI int32_t getN(int i) const {
+    if (i < STK_LDS) return ldsN()[i * 64 + threadIdx.x];
+    return sN[i - STK_LDS];
+  }
+  DEVI void setN(int i, int32_t v) {
+    if (i < STK_LDS) ldsN()[i * 64 + threadIdx.x] = v;
+    else sN[i - STK_LDS] = v;
+  }
+};
+struct NStack {  // shadow traversal: node indices only
+  int32_t sN[BVH_STACK - STK_LDS];
+  DEVI int32_t getN(int i) const {
+    if (i < STK_LDS) return ldsN()[i * 64 + threadIdx.x];
+    return sN[i - STK_LDS];
+  }
+  DEVI void setN(int i, int32_t v) {
+    if (i < STK_LDS) ldsN()[i * 64 + threadIdx.x] = v;
+    else sN[i - STK_LDS] = v;
+  }
+};
+
 // myAccelStruct.intersectCheck + myBVH.traverseStruct (myGeomBase.java:216-222, 407-421),
 // iteratively with the reference's LOCAL pruning: the right child is visited iff its
 // box is hit and (left subtree missed or box entry t < the LEFT SUBTREE's minimal t);
 // ties go left. A frame = the enclosing subtree's minimal t so far + node<<1|phase; the
 // right box is tested when the left subtree is done, as the Java does.
 template <bool CNT, uint32_t F>
-DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, int top, Best& best,
-                        Counters& ct) {
-  double stT[BVH_STACK];
-  int32_t stN[BVH_STACK];
+DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, const RayInv& ri, WRay& w, const Key& k, int top,
+                        Best& best, Counters& ct) {
+  Stack st;
   int sp = 0;
   double local = DMAX;
   int32_t N = A.root;  // a leaf root (a plain list) is tested by the same loop with no frames
@@ -104,30 +151,30 @@ DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, c
     while (N >= 0) {
       const NodeD& nd = S.node[N];
       if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }  // both child boxes are tested once per visit
-      stT[sp] = local;
-      stN[sp] = N << 1;
+      st.setT(sp, local);
+      st.setN(sp, N << 1);
       sp++;
       local = DMAX;
       double tL;
-      if (slab(nd.lmin, nd.lmax, ao, ad, tL)) N = nd.left;
+      if (slab(nd.lmin, nd.lmax, ao, ad, ri, tL)) N = nd.left;
       else { N = INT32_MAX; break; }
     }
     if (N != INT32_MAX) leaf_closest<CNT, F>(S, ~N, A.xf, ao, ad, w, k, top, best, local, ct);
     // unwind
     N = INT32_MAX;
     while (sp > 0) {
-      const int32_t np = stN[sp - 1];
+      const int32_t np = st.getN(sp - 1);
       if ((np & 1) == 0) {
         const NodeD& nd = S.node[np >> 1];
         double tR;
-        if (slab(nd.rmin, nd.rmax, ao, ad, tR) && (local == DMAX || tR < local)) {
-          stN[sp - 1] = np | 1;
+        if (slab(nd.rmin, nd.rmax, ao, ad, ri, tR) && (local == DMAX || tR < local)) {
+          st.setN(sp - 1, np | 1);
           N = nd.right;
           break;
         }
       }
       // this node's minimal t joins the enclosing subtree's
-      const double sv = stT[sp - 1];
+      const double sv = st.getT(sp - 1);
       if (sv < local) local = sv;
       sp--;
     }
@@ -148,10 +195,11 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
     if (tp.kind == TOP_ACCEL) {
       const AccelD& A = S.accel[tp.idx];
       if (CNT) { ct.c[C_ROOT]++; ct.c[C_BOX]++; }
+      RayInv ri = ray_inv(o, d, S.fastSlab);
       double te;
-      if (!slab(A.bmin, A.bmax, o, d, te)) continue;
+      if (!slab(A.bmin, A.bmax, o, d, ri, te)) continue;
       w.moved = false;
-      accel_closest<CNT, F>(S, A, o, d, w, k, i, best, ct);
+      accel_closest<CNT, F>(S, A, o, d, ri, w, k, i, best, ct);
     } else {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
@@ -167,10 +215,10 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
 // any-hit: mySceneObject/myBBox/myGeomList/myBVH.calcShadowHit (mySceneObject.java:33-38,
 // myGeomBase.java:166-170, 268-277, 397-404): blocked iff hit && dist - t > 1e-7
 template <bool CNT>
-DEVI bool shadow_box(const double* mn, const double* mx, V o, V d, double dist, Counters& ct) {
+DEVI bool shadow_box(const double* mn, const double* mx, V o, V d, const RayInv& ri, double dist, Counters& ct) {
   if (CNT) ct.c[C_BOX]++;
   double te;
-  return slab(mn, mx, o, d, te) && (dist - te) > EPS;
+  return slab(mn, mx, o, d, ri, te) && (dist - te) > EPS;
 }
 template <bool CNT, uint32_t F>
 DEVI bool leaf_any(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
@@ -191,24 +239,25 @@ DEVI bool leaf_any(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, co
 }
 template <bool CNT, uint32_t F>
 DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
-  int32_t stk[BVH_STACK];
+  const RayInv ri = ray_inv(ao, ad, S.fastSlab);
+  NStack st;
   int sp = 0;
   int32_t N = A.root;
   // leafVals.calcShadowHit tests its own box first; myBVH.calcShadowHit (internal) does not
-  if (N < 0 && !shadow_box<CNT>(A.bmin, A.bmax, ao, ad, dist, ct)) return false;
+  if (N < 0 && !shadow_box<CNT>(A.bmin, A.bmax, ao, ad, ri, dist, ct)) return false;
   while (true) {
     if (N >= 0) {  // internal: push (right child pending), go left if its box is hit
       const NodeD& nd = S.node[N];
       if (CNT) ct.c[C_NODE]++;
-      stk[sp++] = N;
-      if (shadow_box<CNT>(nd.lmin, nd.lmax, ao, ad, dist, ct)) { N = nd.left; continue; }
+      st.setN(sp++, N);
+      if (shadow_box<CNT>(nd.lmin, nd.lmax, ao, ad, ri, dist, ct)) { N = nd.left; continue; }
     } else if (N != INT32_MAX) {
       if (leaf_any<CNT, F>(S, ~N, A.xf, ao, ad, w, k, dist, ct)) return true;
     }
     N = INT32_MAX;
     while (sp > 0) {
-      const NodeD& pn = S.node[stk[--sp]];
-      if (shadow_box<CNT>(pn.rmin, pn.rmax, ao, ad, dist, ct)) { N = pn.right; break; }
+      const NodeD& pn = S.node[st.getN(--sp)];
+      if (shadow_box<CNT>(pn.rmin, pn.rmax, ao, ad, ri, dist, ct)) { N = pn.right; break; }
     }
     if (N == INT32_MAX) return false;
   }
@@ -872,7 +921,7 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
 }
 
 #ifndef RT_RENDER_WAVES
-#define RT_RENDER_WAVES 5
+#define RT_RENDER_WAVES 4
 #endif
 template <bool CNT, uint32_t F>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_RENDER_WAVES)))
@@ -882,7 +931,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   // loads, little divergence). Lane j of a pixel traces samples j, j+G, ...; each round's
   // G colours go through LDS and the pixel's first lane adds them in sample order, so
   // the per-pixel sum is the reference's sequential sum (myScene.java:1451-1460).
-  __shared__ double cbuf[64 * 3];
+  double* cbuf = rt_lds;  // 64 x 3 doubles, aliases the traversal stack
   const int lane = threadIdx.x;
   const int G = P.G;
   const int j = lane & (G - 1), pl = lane / G;

@@ -1,13 +1,22 @@
 #!/bin/bash
-# Tuning session on the GPU box: sweep of tools/_variants builds + one PMC pass of the default build.
+# Tuning session on the GPU box: sweep of tools/_variants builds + PMC passes of the default build.
 set -o pipefail
 TAG=${1:-perf}
 NAMES=${2:-w2,w3,w4}
+PASSES=${3:-sq}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python3 tools/variant_sweep.py run --names $NAMES > $OUT/sweep.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d $OUT/pmc_sq -o run -- python3 tools/variant_sweep.py one --iters 1 > $OUT/pmc_sq.log 2>&1
-rc=$?
+declare -A PMC
+PMC[sq]="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS"
+PMC[mem]="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_INST_LEVEL_VMEM SQ_IFETCH SQC_ICACHE_MISSES SQ_LEVEL_WAVES TCC_HIT_sum TCC_MISS_sum"
+PMC[tcp]="TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_WRITE_REQ_sum TCP_PENDING_STALL_CYCLES_sum"
+PMC[fetch]="FETCH_SIZE"
+rc=0
+timeout -k 10 600 python3 tools/variant_sweep.py run --names $NAMES > $OUT/sweep.log 2>&1 || rc=$?
+for p in ${PASSES//,/ }; do
+  [ $rc -ne 0 ] && break
+  timeout -k 10 300 rocprofv3 --pmc ${PMC[$p]} --output-format csv -d $OUT/pmc_$p -o run -- python3 tools/variant_sweep.py one --iters 1 > $OUT/pmc_$p.log 2>&1 || rc=$?
+done
 echo "chain exit $rc" >> $OUT/status.txt
 exit $rc

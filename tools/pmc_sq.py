@@ -3,12 +3,14 @@
 import csv
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
+rows = []
+for f in sys.argv[1:]:
+    rows += list(csv.DictReader(open(f)))
 agg = {}
 for r in rows:
     if "render_kernel" not in r["Kernel_Name"]:
         continue
-    agg.setdefault(r["Dispatch_Id"], {})[r["Counter_Name"]] = float(r["Counter_Value"])
+    agg.setdefault(r["Kernel_Name"][:40] + "#" + r["Dispatch_Id"] if len(sys.argv) == 2 else r["Kernel_Name"][:40], {})[r["Counter_Name"]] = float(r["Counter_Value"])
 for d, v in agg.items():
     wc = v.get("SQ_WAVE_CYCLES", 1)
     print(d, {k: f"{x:.3g}" for k, x in v.items()})

@@ -19,22 +19,30 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 OUT = REPO / "tools" / "_variants"
-VARIANTS = {  # name -> -D defines
-    "w1": ["RT_RENDER_WAVES=1"],
-    "w2": ["RT_RENDER_WAVES=2"],
-    "w3": ["RT_RENDER_WAVES=3"],
-    "w4": ["RT_RENDER_WAVES=4"],
-    "w5": ["RT_RENDER_WAVES=5"],
-    "w6": ["RT_RENDER_WAVES=6"],
-    "w8": ["RT_RENDER_WAVES=8"],
-}
+VARIANTS = {}  # name -> -D defines; names like "s12w4" are parsed (see defines_of)
+FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS"}
+
+
+def defines_of(name: str) -> list[str]:
+    import re
+    if name in VARIANTS:
+        return VARIANTS[name]
+    return [f"{FIELDS[k]}={v}" for k, v in re.findall(r"([a-z])(\d+)", name)]
+
+
+def _build_one(n):
+    from distraytracer_old_amd import build
+    p = build.build(defines=defines_of(n), out=OUT / f"lib_{n}.so")
+    for o in OUT.glob(f"lib_{n}.*.o"):
+        o.unlink()
+    return p
 
 
 def do_build(names):
-    from distraytracer_old_amd import build
-    for n in names:
-        p = build.build(defines=VARIANTS[n], out=OUT / f"lib_{n}.so")
-        print("built", p, flush=True)
+    from concurrent.futures import ProcessPoolExecutor
+    with ProcessPoolExecutor(max_workers=4) as ex:
+        for p in ex.map(_build_one, names):
+            print("built", p, flush=True)
 
 
 def time_one(cfg: str, W: int, H: int, spp: int, iters: int, flags: int):
@@ -53,7 +61,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("mode", choices=["build", "run", "one"])
     ap.add_argument("--cfg", default="C3")
-    ap.add_argument("--names", default=",".join(VARIANTS))
+    ap.add_argument("--names", default="w4,w5")
     ap.add_argument("--W", type=int, default=0)
     ap.add_argument("--H", type=int, default=0)
     ap.add_argument("--spp", type=int, default=0)
