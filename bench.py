@@ -38,19 +38,18 @@ sys.path.insert(0, str(REPO))
 METRIC = "Mray/s + achieved HBM GB/s, bun69k.cli 1024² 16spp, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
-# record bytes per counted event (rt_types.h layouts; DESIGN.md "Algorithmic bytes")
+# Algorithmic bytes per counted event: SURVEY.md 8(d)'s per-ray formula, records at the
+# sizes it states and no cache credit:
+#   64 node + 48 triangle + 64 quad + 32 sphere/cylinder + 16 light + 32 photon kd-node
+#   + 16 texel quad (DESIGN.md "Measurement")
 RECORD_BYTES = {
-    "node": 128,      # NodeD: both child boxes of an internal node
-    "tri": 128,       # TriD
-    "quad": 256,      # PrimD (planar)
-    "implicit": 256,  # PrimD (sphere / cylinder / box)
-    "leaf": 8,        # LeafD
-    "member": 4,      # leaf member ref
-    "root": 64,       # AccelD root box
-    "top": 16 + 96,   # TopD + the 3 used rows of the inverse CTM
-    "light": 272,     # LightD
-    "photon": 64,     # PhotonD
-    "texel": 16,      # 4 texels of a bilinear lookup
+    "node": 64,       # BVH node records fetched (internal-node visits)
+    "tri": 48,        # triangle records tested
+    "quad": 64,       # quad / plane records tested
+    "implicit": 32,   # sphere / cylinder / box records tested
+    "light": 16,      # light records read per shaded hit
+    "photon": 32,     # photon kd-nodes visited
+    "texel": 16,      # bilinear texel quads fetched
 }
 
 

@@ -54,6 +54,13 @@ struct NodeD {
 struct LeafD {
   int32_t start, count;  // range in leaf member refs (>= 0 tri index, < 0 ~prim index)
 };
+// Child references (NodeD.left/right, AccelD.root): >= 0 node index; < 0: c = ~ref is a
+// leaf, either a LeafD index (bit 30 clear) or, with LEAF_RUN_FLAG, a run of `count`
+// consecutive triangles starting at `start` (scene_build.cpp pack_leaves).
+static constexpr int32_t LEAF_RUN_FLAG = 1 << 30;
+static constexpr int32_t LEAF_RUN_MAXCOUNT = 31;
+static constexpr int32_t LEAF_RUN_MAXSTART = (1 << 25) - 1;
+inline int32_t leaf_run_ref(int32_t start, int32_t count) { return ~(LEAF_RUN_FLAG | (start << 5) | count); }
 // A myBVH or a myGeomList (one leaf holding the whole list).
 struct AccelD {
   double bmin[3], bmax[3];  // root box (list box / BVH root box)

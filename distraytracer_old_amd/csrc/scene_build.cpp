@@ -436,11 +436,51 @@ struct Builder {
   }
 };
 
+// Renumber triangles in leaf order so that a leaf whose members are all triangles holds
+// a consecutive run; such a leaf is then encoded in its parent's child reference
+// (LEAF_RUN, rt_types.h) and the kernel reads no LeafD and no member index for it --
+// two dependent loads fewer per leaf visit. Visit order and all results are unchanged.
+void pack_leaves(HostScene& hs) {
+  const int nt = (int)hs.tri.size();
+  std::vector<int32_t> perm(nt, -1);  // old -> new
+  std::vector<int32_t> order;         // new -> old
+  order.reserve(nt);
+  for (const LeafD& lf : hs.leaf)
+    for (int i = 0; i < lf.count; ++i) {
+      int32_t r = hs.member[lf.start + i];
+      if (r >= 0 && perm[r] < 0) { perm[r] = (int32_t)order.size(); order.push_back(r); }
+    }
+  for (int r = 0; r < nt; ++r)
+    if (perm[r] < 0) { perm[r] = (int32_t)order.size(); order.push_back(r); }
+  std::vector<TriD> tri(nt);
+  for (int k = 0; k < nt; ++k) tri[k] = hs.tri[order[k]];
+  hs.tri.swap(tri);
+  for (int32_t& r : hs.member)
+    if (r >= 0) r = perm[r];
+  for (TopD& t : hs.top)
+    if (t.kind == TOP_TRI) t.idx = perm[t.idx];
+  // child references of leaves that are consecutive triangle runs
+  auto code = [&](int32_t child) -> int32_t {
+    if (child >= 0) return child;
+    const LeafD& lf = hs.leaf[~child];
+    if (lf.count <= 0 || lf.count > LEAF_RUN_MAXCOUNT) return child;
+    int32_t s0 = hs.member[lf.start];
+    if (s0 < 0 || s0 > LEAF_RUN_MAXSTART) return child;
+    for (int i = 1; i < lf.count; ++i)
+      if (hs.member[lf.start + i] != s0 + i) return child;
+    return leaf_run_ref(s0, lf.count);
+  };
+  for (NodeD& n : hs.node) { n.left = code(n.left); n.right = code(n.right); }
+  for (AccelD& a : hs.accel) a.root = code(a.root);
+}
+
 }  // namespace
 
 int build_host_scene(const rt_scene_desc* d, HostScene& hs) {
   Builder b(d, hs);
   if (!b.run()) return set_error(RT_E_INVALID, b.err);
+  if (hs.leaf.size() >= (size_t)LEAF_RUN_FLAG) return set_error(RT_E_INVALID, "too many BVH leaves");
+  pack_leaves(hs);
   return RT_OK;
 }
 

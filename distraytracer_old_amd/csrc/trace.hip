@@ -239,7 +239,7 @@ static RenderFn pick_variant(const HostScene& h, uint32_t flags) {
 static int launch(rt_scene* s, const ParamsD& P, uint32_t flags, float* d_rgb, int32_t* d_argb, bool count,
                   hipStream_t st) {
   int tilesX = (P.W + P.tw - 1) / P.tw, tilesY = (P.nrows + P.th - 1) / P.th;
-  dim3 grid(tilesX * tilesY), block(64);
+  dim3 grid(dv::xcd_grid(tilesX * tilesY)), block(64);
   if (count) {  // counting always runs the all-features kernel
     HIPCHK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long) * RT_ST_N, st));
     hipLaunchKernelGGL((dv::render_kernel<true, dv::FT_ALL>), grid, block, dv::LDS_BYTES, st, s->dev, P, d_rgb, d_argb,

@@ -63,13 +63,27 @@ DEVI int32_t ref_xf(const SceneD& S, int32_t ref) { return (!(F & FT_PRIM) || re
 // needs each subtree's minimal t -- a double per stack frame.
 
 // myGeomList.traverseStruct leaf loop (myGeomBase.java:281-296): strict <, leaf order
+// a leaf from its child code c = ~ref (rt_types.h): a LeafD or a packed triangle run
+struct LeafR {
+  int32_t start, count;
+  bool run;
+};
+DEVI LeafR leaf_of(const SceneD& S, int32_t c) {
+  LeafR r;
+  r.run = (c & LEAF_RUN_FLAG) != 0;
+  if (r.run) { r.start = (c >> 5) & LEAF_RUN_MAXSTART; r.count = c & 31; }
+  else { LeafD lf = S.leaf[c]; r.start = lf.start; r.count = lf.count; }
+  return r;
+}
+DEVI int32_t leaf_member(const SceneD& S, const LeafR& lf, int i) { return lf.run ? lf.start + i : S.member[lf.start + i]; }
+
 template <bool CNT, uint32_t F>
-DEVI void leaf_closest(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, const Key& k, int top, Best& best,
+DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w, const Key& k, int top, Best& best,
                        double& local, Counters& ct) {
-  LeafD lf = S.leaf[leaf];
+  const LeafR lf = leaf_of(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
   for (int i = 0; i < lf.count; ++i) {
-    int32_t ref = S.member[lf.start + i];
+    int32_t ref = leaf_member(S, lf, i);
     renorm(w);  // _ray.getTransformedRay(_ray, obj.CTMara[invIDX])
     int xf = ref_xf<F>(S, ref);
     V o, d;
@@ -221,11 +235,11 @@ DEVI bool shadow_box(const double* mn, const double* mx, V o, V d, const RayInv&
   return slab(mn, mx, o, d, ri, te) && (dist - te) > EPS;
 }
 template <bool CNT, uint32_t F>
-DEVI bool leaf_any(const SceneD& S, int leaf, int accXf, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
-  LeafD lf = S.leaf[leaf];
+DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
+  const LeafR lf = leaf_of(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
   for (int i = 0; i < lf.count; ++i) {
-    int32_t ref = S.member[lf.start + i];
+    int32_t ref = leaf_member(S, lf, i);
     renorm(w);
     int xf = ref_xf<F>(S, ref);
     V o, d;
@@ -920,6 +934,27 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
   }
 }
 
+// XCD-aware tile order. Workgroups are dealt round-robin to the 8 XCDs (block b -> XCD
+// b % 8), each with its own L2. With XCD_CHUNKS = k > 0 the row-major tile list is cut
+// into 8k contiguous chunks and XCD x renders chunks x, x+8, ...: each L2 then sees a
+// few image bands (and the part of the scene they show) instead of the whole frame.
+#ifndef RT_XCD_CHUNKS
+#define RT_XCD_CHUNKS 0
+#endif
+static constexpr int XCD_CHUNKS = RT_XCD_CHUNKS;
+__host__ __device__ inline int xcd_grid(int ntiles) {
+  if (XCD_CHUNKS == 0) return ntiles;
+  const int nch = 8 * XCD_CHUNKS, csz = (ntiles + nch - 1) / nch;
+  return nch * csz;
+}
+DEVI int tile_of_block(int b, int ntiles) {
+  if (XCD_CHUNKS == 0) return b;
+  const int nch = 8 * XCD_CHUNKS, csz = (ntiles + nch - 1) / nch;
+  const int xcd = b & 7, slot = b >> 3;
+  const int t = ((slot / csz) * 8 + xcd) * csz + slot % csz;
+  return t < ntiles ? t : -1;
+}
+
 #ifndef RT_RENDER_WAVES
 #define RT_RENDER_WAVES 4
 #endif
@@ -936,7 +971,9 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   const int G = P.G;
   const int j = lane & (G - 1), pl = lane / G;
   const int tilesX = (P.W + P.tw - 1) / P.tw;
-  const int tx = blockIdx.x % tilesX, ty = blockIdx.x / tilesX;
+  const int tile = tile_of_block(blockIdx.x, tilesX * ((P.nrows + P.th - 1) / P.th));
+  if (tile < 0) return;  // padding block of the XCD mapping (whole workgroup)
+  const int tx = tile % tilesX, ty = tile / tilesX;
   const int col = tx * P.tw + pl % P.tw;
   const int ri = ty * P.th + pl / P.tw;  // row index within this render's rows
   const bool valid = col < P.W && ri < P.nrows;

@@ -24,7 +24,8 @@ if pmc_csv != "-":
             name = r.get("Kernel_Name", "")
             per[name].append(float(r["Counter_Value"]))
     res["fetch_size_kb"] = {k: v for k, v in per.items()}
-    kern = [k for k in per if "render_kernel<false>" in k or ("render_kernel" in k and "ILb0" in k)]
+    # the timed (non-counting) render kernel: the variant launched most often
+    kern = sorted([k for k in per if "render_kernel<false" in k], key=lambda k: -len(per[k]))
     if kern:
         vals = per[kern[0]]
         kb = sum(vals) / len(vals)

@@ -20,7 +20,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 OUT = REPO / "tools" / "_variants"
 VARIANTS = {}  # name -> -D defines; names like "s12w4" are parsed (see defines_of)
-FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS"}
+FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS"}
 
 
 def defines_of(name: str) -> list[str]:
