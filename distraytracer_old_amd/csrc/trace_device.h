@@ -174,10 +174,72 @@ DEVI bool slab_t(const double* mn, const double* mx, V o, V d, const double* y, 
 DEVI bool slab(const double* mn, const double* mx, V o, V d, double& tEntry) {
   return slab_t<false>(mn, mx, o, d, nullptr, tEntry);
 }
-DEVI bool slab(const double* mn, const double* mx, V o, V d, const RayInv& ri, double& tEntry) {
+// ---- box tests on the traversal hot path --------------------------------------------
+// With a valid RayInv (ri.fast) every slab t is first approximated as t' = RN(a * y),
+// within 2^-51 |t'| of the exact t = RN(a / b) (a = RN(bound - o) as in the exact test).
+// The box decisions only compare slab values (with each other, with 0, with a hit t or a
+// shadow distance), so t' settles a decision whenever the compared quantities are further
+// apart than a 2^-46 relative margin; otherwise (grazing rays) the exact test decides.
+// The sign of every t' equals the sign of t (no underflow in the qdiv ranges), so
+// "entry > 0" is always settled exactly.
+static constexpr double APX = 0x1p-46;
+DEVI int slab_apx(const double* mn, const double* mx, V o, const double* y, double& lo) {
+  const double b0 = mn[0], b1 = mn[1], b2 = mn[2], b3 = mx[0], b4 = mx[1], b5 = mx[2];
+  const double t0 = (b0 - o.x) * y[0], t3 = (b3 - o.x) * y[0];
+  const double t1 = (b1 - o.y) * y[1], t4 = (b4 - o.y) * y[1];
+  const double t2 = (b2 - o.z) * y[2], t5 = (b5 - o.z) * y[2];
+  lo = fmax(fmax(fmin(t0, t3), fmin(t1, t4)), fmin(t2, t5));
+  const double hi = fmin(fmin(fmax(t0, t3), fmax(t1, t4)), fmax(t2, t5));
+  if (!(lo > 0)) return 0;
+  const double diff = hi - lo, tol = APX * (fabs(hi) + fabs(lo));
+  if (diff > tol) return 1;
+  if (-diff > tol) return 0;
+  return -1;
+}
+DEVI bool slab_exact(const double* mn, const double* mx, V o, V d, const RayInv& ri, double& tEntry) {
   if (ri.fast) return slab_t<true>(mn, mx, o, d, ri.y, tEntry);
   return slab_t<false>(mn, mx, o, d, nullptr, tEntry);
 }
+// hit?  (myBBox.intersectCheck != null)
+DEVI bool box_hit(const double* mn, const double* mx, V o, V d, const RayInv& ri) {
+  double te;
+  if (ri.fast) {
+    int r = slab_apx(mn, mx, o, ri.y, te);
+    if (r >= 0) return r != 0;
+  }
+  return slab_exact(mn, mx, o, d, ri, te);
+}
+// hit and (lim == DMAX or entry t < lim)   (BVH right-child rule)
+DEVI bool box_before(const double* mn, const double* mx, V o, V d, const RayInv& ri, double lim) {
+  double te;
+  if (ri.fast) {
+    int r = slab_apx(mn, mx, o, ri.y, te);
+    if (r == 0) return false;
+    if (r == 1) {
+      if (lim == DMAX) return true;
+      const double tol = APX * (fabs(te) + fabs(lim));
+      if (lim - te > tol) return true;
+      if (te - lim > tol) return false;
+    }
+  }
+  if (!slab_exact(mn, mx, o, d, ri, te)) return false;
+  return lim == DMAX || te < lim;
+}
+// hit and dist - entry t > 1e-7   (calcShadowHit on a box)
+DEVI bool box_shadow(const double* mn, const double* mx, V o, V d, const RayInv& ri, double dist) {
+  double te;
+  if (ri.fast) {
+    int r = slab_apx(mn, mx, o, ri.y, te);
+    if (r == 0) return false;
+    if (r == 1) {
+      const double g = (dist - te) - EPS, tol = APX * (fabs(te) + fabs(dist));
+      if (g > tol) return true;
+      if (-g > tol) return false;
+    }
+  }
+  return slab_exact(mn, mx, o, d, ri, te) && (dist - te) > EPS;
+}
+
 DEVI int slab_plane(const double* mn, const double* mx, V o, V d) {  // plane idx for myBBox normals
   double ro[3] = {o.x, o.y, o.z}, rd[3] = {d.x, d.y, d.z};
   double biggestMin = -DMAX;
@@ -191,8 +253,25 @@ DEVI int slab_plane(const double* mn, const double* mx, V o, V d) {  // plane id
 }
 
 // planar: orientation with N.d < 0 (the reference flips the vertex order in place, Q5)
-template <int NV, bool PLANE>
-DEVI bool planar_test(const double (*v)[3], V nA, V nB, double dA, double dB, V o, V d, double& t, int& st) {
+// Hit filters: a candidate whose t cannot change the caller's outcome may be reported as a
+// miss without running the inside test (the decision it would feed is already fixed):
+// closest hit -- t neither below the subtree minimum nor below the running best;
+// shadow -- not (dist - t > 1e-7). LimNone: the full test (hit records, photons).
+struct LimNone {
+  DEVI bool ok(double) const { return true; }
+};
+struct LimClosest {
+  double a, b;
+  DEVI bool ok(double t) const { return t < a || t < b; }
+};
+struct LimShadow {
+  double dist;
+  DEVI bool ok(double t) const { return (dist - t) > EPS; }
+};
+
+template <int NV, bool PLANE, class LIM = LimNone>
+DEVI bool planar_test(const double (*v)[3], V nA, V nB, double dA, double dB, V o, V d, double& t, int& st,
+                      const LIM& lim = LIM()) {
   double pr = dot(nA, d);
   if (!(fabs(pr) > 0)) return false;
   V N;
@@ -207,6 +286,7 @@ DEVI bool planar_test(const double (*v)[3], V nA, V nB, double dA, double dB, V 
   t = -(dot(N, o) + D) / pr;
   if (!(t > EPS)) return false;
   if (PLANE) return true;
+  if (!lim.ok(t)) return false;
   V p = mk(d.x * t + o.x, d.y * t + o.y, d.z * t + o.z);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {  // checkInside (myPlanarObject.java:165-175, 200-211)
@@ -220,10 +300,11 @@ DEVI bool planar_test(const double (*v)[3], V nA, V nB, double dA, double dB, V 
   return true;
 }
 
-DEVI bool tri_test(const TriD& T, V o, V d, double& t, int& st) {
+template <class LIM = LimNone>
+DEVI bool tri_test(const TriD& T, V o, V d, double& t, int& st, const LIM& lim = LIM()) {
   V nA = ld3(T.n);
   V nB = mk(-nA.x, -nA.y, -nA.z);  // exactly the reversed-order normal
-  return planar_test<3, false>(T.v, nA, nB, T.dA, T.dB, o, d, t, st);
+  return planar_test<3, false>(T.v, nA, nB, T.dA, T.dB, o, d, t, st, lim);
 }
 
 DEVI V sphere_center(const PrimD& P, const Key& k) {

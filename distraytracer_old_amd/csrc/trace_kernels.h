@@ -43,11 +43,12 @@ struct Best {
 };
 DEVI Best miss() { Best b; b.t = DMAX; b.ref = 0; b.top = -1; b.ver = 0; b.inAcc = 0; return b; }
 
-template <bool CNT, uint32_t F>
-DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, double& t, int& args, Counters& ct) {
+template <bool CNT, uint32_t F, class LIM = LimNone>
+DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, double& t, int& args, Counters& ct,
+                   const LIM& lim = LIM()) {
   if (!(F & FT_PRIM) || ref >= 0) {
     if (CNT) ct.c[C_TRI]++;
-    return tri_test(S.tri[ref], o, d, t, args);
+    return tri_test(S.tri[ref], o, d, t, args, lim);
   }
   const PrimD& P = S.prim[~ref];
   if (CNT) { if (P.type == PT_QUAD || P.type == PT_PLANE) ct.c[C_QUAD]++; else ct.c[C_IMPLICIT]++; }
@@ -91,7 +92,7 @@ DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRa
     else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
     double t;
     int args;
-    if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct)) {
+    if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, LimClosest{local, best.t})) {
       if (t < local) local = t;
       if (t < best.t) { best.t = t; best.ref = ref; best.ver = w.ver; best.top = (int16_t)top; best.inAcc = 1; }
     }
@@ -169,8 +170,7 @@ DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, const RayI
       st.setN(sp, N << 1);
       sp++;
       local = DMAX;
-      double tL;
-      if (slab(nd.lmin, nd.lmax, ao, ad, ri, tL)) N = nd.left;
+      if (box_hit(nd.lmin, nd.lmax, ao, ad, ri)) N = nd.left;
       else { N = INT32_MAX; break; }
     }
     if (N != INT32_MAX) leaf_closest<CNT, F>(S, ~N, A.xf, ao, ad, w, k, top, best, local, ct);
@@ -180,8 +180,7 @@ DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, const RayI
       const int32_t np = st.getN(sp - 1);
       if ((np & 1) == 0) {
         const NodeD& nd = S.node[np >> 1];
-        double tR;
-        if (slab(nd.rmin, nd.rmax, ao, ad, ri, tR) && (local == DMAX || tR < local)) {
+        if (box_before(nd.rmin, nd.rmax, ao, ad, ri, local)) {
           st.setN(sp - 1, np | 1);
           N = nd.right;
           break;
@@ -210,15 +209,14 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       const AccelD& A = S.accel[tp.idx];
       if (CNT) { ct.c[C_ROOT]++; ct.c[C_BOX]++; }
       RayInv ri = ray_inv(o, d, S.fastSlab);
-      double te;
-      if (!slab(A.bmin, A.bmax, o, d, ri, te)) continue;
+      if (!box_hit(A.bmin, A.bmax, o, d, ri)) continue;
       w.moved = false;
       accel_closest<CNT, F>(S, A, o, d, ri, w, k, i, best, ct);
     } else {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
       int args;
-      if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct) && t < best.t) {
+      if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, LimClosest{best.t, best.t}) && t < best.t) {
         best.t = t; best.ref = ref; best.top = (int16_t)i; best.inAcc = 0; best.ver = w.ver;
       }
     }
@@ -231,8 +229,7 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
 template <bool CNT>
 DEVI bool shadow_box(const double* mn, const double* mx, V o, V d, const RayInv& ri, double dist, Counters& ct) {
   if (CNT) ct.c[C_BOX]++;
-  double te;
-  return slab(mn, mx, o, d, ri, te) && (dist - te) > EPS;
+  return box_shadow(mn, mx, o, d, ri, dist);
 }
 template <bool CNT, uint32_t F>
 DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
@@ -247,7 +244,7 @@ DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w
     else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
     double t;
     int args;
-    if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct) && (dist - t) > EPS) return true;
+    if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, LimShadow{dist}) && (dist - t) > EPS) return true;
   }
   return false;
 }
@@ -293,7 +290,7 @@ DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
       int args;
-      if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct) && (dist - t) > EPS) return true;
+      if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, LimShadow{dist}) && (dist - t) > EPS) return true;
     }
   }
   return false;
@@ -678,6 +675,9 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     if (CNT) ct.c[C_SHADOW]++;
     Key sk = k;
     sk.tsite = SITE_SHADOW_TIME + li;
+#ifdef RT_PROF_NOSHADOW  // profiling builds only (tools/variant_sweep.py): results differ
+    if (false)
+#endif
     if (shadowed<CNT, F>(S, sr, sk, t, ct)) continue;
     renorm(sr);  // shadowRay.direction._normalize()
     double ldp = dot(sr.d, h.nrm) * ltMult;
@@ -805,6 +805,9 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
   Fr.local = mk(r, g, b);
   if constexpr ((F & FT_TRANS) != 0) Fr.acc = mk(0, 0, 0);
   branch = (in.gen < S.numRays - 2) && m.hasCaustic;
+#ifdef RT_PROF_NOSECONDARY  // profiling builds only: results differ
+  branch = false;
+#endif
   if (!branch) return 0;
   a.o = h.fwd;
   a.gen = in.gen + 1;

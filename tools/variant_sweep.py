@@ -19,7 +19,11 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 OUT = REPO / "tools" / "_variants"
-VARIANTS = {}  # name -> -D defines; names like "s12w4" are parsed (see defines_of)
+VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_of)
+    "noshadow": ["RT_PROF_NOSHADOW"],          # profiling only: results differ
+    "nosec": ["RT_PROF_NOSECONDARY"],
+    "primary": ["RT_PROF_NOSHADOW", "RT_PROF_NOSECONDARY"],
+}
 FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS"}
 
 
