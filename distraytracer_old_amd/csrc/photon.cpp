@@ -1,8 +1,16 @@
-// Photon kd-tree build on the host (myKD_Tree.build_tree, myLight.java:325-381):
-// split axis = largest extent (ties x, then y, z), Collections.sort (stable) on
-// that axis, median = size/2 stored at the node, children [0,split) and
-// (split, size). Input order = the reference's photon_list insertion order.
+// Photon-map search structure (host). The reference stores photon_list in a
+// one-photon-per-node kd-tree (myKD_Tree.build_tree, myLight.java:325-381) and
+// answers getIrradianceFromPhtnTree (myObjShader.java:441-458) with the k nearest
+// photons within max_dist. That set is a property of the photon list, not of the
+// tree, so the device uses a structure that suits 64-wide waves: a BVH whose leaves
+// are ranges of <= PHOTON_LEAF photons stored contiguously (positions / powers as
+// double[3] in leaf order) -- a query walks ~log2(n/24) nodes and scans whole
+// leaves instead of chasing one dependent pointer per photon.
+//
+// Build: median partition of the photon index range on the axis of largest extent
+// (order by (coordinate, index)), boxes from the photons' exact coordinates.
 #include <algorithm>
+#include <cstring>
 #include <utility>
 
 #include "rt_internal.h"
@@ -10,52 +18,49 @@
 namespace rt {
 namespace {
 
-struct KdBuilder {
+struct PhotonBvh {
   const std::vector<double>& pos;
-  const std::vector<double>& pwr;
-  std::vector<PhotonD>& nodes;
-  std::vector<std::pair<double, int>> tmp;
+  std::vector<int>& idx;
+  std::vector<NodeD>& nodes;
 
-  int build(std::vector<int>& idx, int lo, int hi) {
-    int sz = hi - lo;
-    PhotonD n;
-    std::memset(&n, 0, sizeof(n));
-    if (sz == 1) {
-      int p = idx[lo];
-      for (int c = 0; c < 3; ++c) { n.pos[c] = pos[3 * p + c]; n.pwr[c] = pwr[3 * p + c]; }
-      n.axis = -1; n.left = n.right = -1;
-      nodes.push_back(n);
-      return (int)nodes.size() - 1;
-    }
-    double mins[3] = {1e20, 1e20, 1e20}, maxs[3] = {-1e20, -1e20, -1e20};
-    for (int i = lo; i < hi; i++) {
-      const double* q = &pos[3 * idx[i]];
-      for (int j = 0; j < 3; j++) {
-        if (q[j] < mins[j]) mins[j] = q[j];
-        if (q[j] > maxs[j]) maxs[j] = q[j];
+  void box(int lo, int hi, double* mn, double* mx) const {
+    for (int c = 0; c < 3; ++c) { mn[c] = 1e300; mx[c] = -1e300; }
+    for (int i = lo; i < hi; ++i) {
+      const double* q = &pos[3 * (size_t)idx[i]];
+      for (int c = 0; c < 3; ++c) {
+        mn[c] = std::min(mn[c], q[c]);
+        mx[c] = std::max(mx[c], q[c]);
       }
     }
-    double dx = maxs[0] - mins[0], dy = maxs[1] - mins[1], dz = maxs[2] - mins[2];
-    int ax = 2;
-    if (dx >= dy && dx >= dz) ax = 0;
-    else if (dy >= dx && dy >= dz) ax = 1;
-    tmp.resize(sz);
-    for (int i = 0; i < sz; ++i) tmp[i] = std::make_pair(pos[3 * idx[lo + i] + ax], idx[lo + i]);
-    std::stable_sort(tmp.begin(), tmp.end(), [](const std::pair<double, int>& a, const std::pair<double, int>& b) {
-      return a.first < b.first;
-    });
-    for (int i = 0; i < sz; ++i) idx[lo + i] = tmp[i].second;
-    int split = sz / 2;
-    int p = idx[lo + split];
-    for (int c = 0; c < 3; ++c) { n.pos[c] = pos[3 * p + c]; n.pwr[c] = pwr[3 * p + c]; }
-    n.axis = ax;
-    int me = (int)nodes.size();
-    nodes.push_back(n);
-    int l = -1, r = -1;
-    if (split != 0) l = build(idx, lo, lo + split);
-    if (split != sz - 1) r = build(idx, lo + split + 1, hi);
-    nodes[me].left = l;
-    nodes[me].right = r;
+  }
+  // Subtree over idx[lo, hi) as a child of its parent: a node index (>= 0), or -1 for a
+  // leaf whose range the parent keeps in NodeD.pad (left: pad[0..1], right: pad[2..3]).
+  int32_t build(int lo, int hi, bool force_node = false) {
+    if (hi - lo <= PHOTON_LEAF && !force_node) return -1;
+    double mn[3], mx[3];
+    box(lo, hi, mn, mx);
+    int ax = 0;
+    for (int c = 1; c < 3; ++c)
+      if (mx[c] - mn[c] > mx[ax] - mn[ax]) ax = c;
+    const int mid = (hi - lo <= PHOTON_LEAF) ? hi : lo + (hi - lo) / 2;  // tiny maps: one leaf + an empty one
+    if (mid < hi)  // median partition on (coordinate, photon index): deterministic
+      std::nth_element(idx.begin() + lo, idx.begin() + mid, idx.begin() + hi, [&](int a, int b) {
+        const double va = pos[3 * (size_t)a + ax], vb = pos[3 * (size_t)b + ax];
+        return va < vb || (va == vb && a < b);
+      });
+    const int me = (int)nodes.size();
+    nodes.push_back(NodeD());
+    const int32_t l = build(lo, mid);
+    const int32_t r = build(mid, hi);
+    NodeD& nd = nodes[me];
+    std::memset(&nd, 0, sizeof(nd));
+    box(lo, mid, nd.lmin, nd.lmax);
+    box(mid, hi, nd.rmin, nd.rmax);
+    nd.left = l;
+    nd.right = r;
+    nd.pad[0] = lo; nd.pad[1] = mid - lo;
+    nd.pad[2] = mid; nd.pad[3] = hi - mid;
+    nd.pad[4] = hi - lo;  // photons in the subtree
     return me;
   }
 };
@@ -63,15 +68,26 @@ struct KdBuilder {
 }  // namespace
 
 void build_photon_tree(HostScene& hs, const std::vector<double>& pos, const std::vector<double>& pwr) {
-  hs.photon.clear();
-  hs.photonRoot = -1;
-  int n = (int)(pos.size() / 3);
+  hs.photonListPos = pos;
+  hs.photonListPwr = pwr;
+  hs.pnode.clear();
+  hs.ppos.clear();
+  hs.ppwr.clear();
+  const int n = (int)(pos.size() / 3);
+  hs.nphoton = n;
+  hs.photonRoot = 0;
   if (n == 0) return;
   std::vector<int> idx(n);
   for (int i = 0; i < n; ++i) idx[i] = i;
-  hs.photon.reserve(n);
-  KdBuilder b{pos, pwr, hs.photon, {}};
-  hs.photonRoot = b.build(idx, 0, n);
+  PhotonBvh b{pos, idx, hs.pnode};
+  hs.photonRoot = b.build(0, n, true);  // the root is always a node
+  hs.ppos.resize(3 * (size_t)n);
+  hs.ppwr.resize(3 * (size_t)n);
+  for (int i = 0; i < n; ++i)
+    for (int c = 0; c < 3; ++c) {
+      hs.ppos[3 * (size_t)i + c] = pos[3 * (size_t)idx[i] + c];
+      hs.ppwr[3 * (size_t)i + c] = pwr[3 * (size_t)idx[i] + c];
+    }
 }
 
 }  // namespace rt

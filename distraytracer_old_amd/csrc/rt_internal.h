@@ -25,8 +25,12 @@ struct HostScene {
   std::vector<LightD> light;
   std::vector<TexD> tex;
   std::vector<uint32_t> texel;
-  std::vector<PhotonD> photon;
-  int photonRoot = -1;
+  // photon map: BVH + leaf-ordered arrays (device layout) and the insertion-order list
+  std::vector<NodeD> pnode;
+  std::vector<double> ppos, ppwr;
+  std::vector<double> photonListPos, photonListPwr;
+  int photonRoot = 0;
+  int64_t nphoton = 0;
   // scene parameters
   double fov = 60;
   double bg[3] = {0, 0, 0};
@@ -42,7 +46,7 @@ struct HostScene {
 };
 
 int build_host_scene(const rt_scene_desc* d, HostScene& hs);  // scene_build.cpp
-// photon.cpp: kd-tree over photons in insertion order (myKD_Tree.build_tree, myLight.java:325-381)
+// photon.cpp: photon-map search structure from the photon_list in insertion order
 void build_photon_tree(HostScene& hs, const std::vector<double>& pos, const std::vector<double>& pwr);
 
 }  // namespace rt

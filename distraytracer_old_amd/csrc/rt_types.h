@@ -104,12 +104,12 @@ struct TexD {
   int64_t off;  // offset into the texel buffer (uint32 0xAARRGGBB)
 };
 
-// photon kd-tree node (myKD_Node + myPhoton, myLight.java:278-298), 64 B
-struct PhotonD {
-  double pos[3];
-  double pwr[3];
-  int32_t axis, left, right, pad;
-};
+// Photon map (myKD_Tree of myPhoton, myLight.java:278-446) on the device: a BVH over the
+// photons (NodeD records; child ref >= 0 node, -1 leaf whose photon range [start,
+// start+count) is in pad[0..1] (left) / pad[2..3] (right); <= 24 photons per leaf) with
+// the photon positions and powers as double[3] arrays in leaf order (csrc/photon.cpp). The k-nearest set a query finds does not depend on the
+// search structure, so this replaces the reference's one-photon-per-node kd-tree.
+static constexpr int PHOTON_LEAF = 24;
 
 // device-side scene handle (all pointers are device pointers)
 struct SceneD {
@@ -125,7 +125,9 @@ struct SceneD {
   const LightD* light;
   const TexD* tex;
   const uint32_t* texel;
-  const PhotonD* photon;
+  const NodeD* pnode;   // photon BVH
+  const double* ppos;   // [nphoton][3], leaf order
+  const double* ppwr;   // [nphoton][3]
   int32_t ntop, nlight, nphoton, photonRoot;
   int32_t photonK;
   double photonMaxD2;

@@ -62,9 +62,10 @@ static int upload_scene(rt_scene* s) {
     return rc;
   d.ntop = (int)h.top.size();
   d.nlight = (int)h.light.size();
-  d.photon = nullptr;
+  d.pnode = nullptr;
+  d.ppos = d.ppwr = nullptr;
   d.nphoton = 0;
-  d.photonRoot = -1;
+  d.photonRoot = 0;
   d.photonK = h.photonK;
   d.photonMaxD2 = h.photonMaxD2;
   for (int c = 0; c < 3; ++c) d.bg[c] = h.bg[c];
@@ -95,12 +96,14 @@ static int upload_scene(rt_scene* s) {
   return RT_OK;
 }
 
-int rt_upload_photons(rt_scene* s) {  // after the host kd-tree build
+int rt_upload_photons(rt_scene* s) {  // after the host photon-map build (csrc/photon.cpp)
   HostScene& h = s->hs;
   HIPCHK(hipSetDevice(s->device));
-  int rc = upload(s, h.photon, &s->dev.photon);
-  if (rc) return rc;
-  s->dev.nphoton = (int)h.photon.size();
+  int rc;
+  if ((rc = upload(s, h.pnode, &s->dev.pnode)) || (rc = upload(s, h.ppos, &s->dev.ppos)) ||
+      (rc = upload(s, h.ppwr, &s->dev.ppwr)))
+    return rc;
+  s->dev.nphoton = (int)h.nphoton;
   s->dev.photonRoot = h.photonRoot;
   s->photonsUploaded = true;
   return RT_OK;
@@ -147,8 +150,21 @@ int rt_scene_info(const rt_scene* s, int64_t* info, int n) {
   const HostScene& h = s->hs;
   int64_t v[12] = {(int64_t)h.top.size(), (int64_t)h.light.size(), h.bvhInternal, h.bvhLeaves, h.bvhDepth,
                    h.bvhPrims, h.nprims, h.rpp, (int64_t)s->devBytes, (int64_t)h.tri.size(),
-                   (int64_t)h.photon.size(), (int64_t)h.mat.size()};
+                   (int64_t)h.nphoton, (int64_t)h.mat.size()};
   for (int i = 0; i < n && i < 12; ++i) info[i] = v[i];
+  return RT_OK;
+}
+
+int rt_scene_photons(const rt_scene* s, double* pos, double* pwr, int64_t n, int64_t* count) {
+  if (!s || !count) return set_error(RT_E_INVALID, "null argument");
+  const HostScene& h = s->hs;
+  *count = h.nphoton;
+  if (n > 0 && (!pos || !pwr)) return set_error(RT_E_INVALID, "null photon buffers");
+  const int64_t m = std::min<int64_t>(n, h.nphoton);
+  if (m > 0) {
+    std::memcpy(pos, h.photonListPos.data(), sizeof(double) * 3 * m);
+    std::memcpy(pwr, h.photonListPwr.data(), sizeof(double) * 3 * m);
+  }
   return RT_OK;
 }
 
@@ -226,6 +242,8 @@ static const Variant kVariants[] = {
     {dv::FT_PRIM, dv::render_kernel<false, dv::FT_PRIM>},
     {dv::FT_PRIM | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX,
      dv::render_kernel<false, dv::FT_PRIM | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX>},
+    {dv::FT_PRIM | dv::FT_TRANS | dv::FT_PHOTON | dv::FT_LIGHTX,
+     dv::render_kernel<false, dv::FT_PRIM | dv::FT_TRANS | dv::FT_PHOTON | dv::FT_LIGHTX>},
     {dv::FT_ALL, dv::render_kernel<false, dv::FT_ALL>},
 };
 

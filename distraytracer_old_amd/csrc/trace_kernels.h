@@ -500,95 +500,276 @@ DEVI V diff_color(const SceneD& S, const MatD& m, const HitRec& h, const Key& k,
 }
 
 // photon kNN gather: myKD_Tree.find_near / findNearbyNodes (myLight.java:389-445) and
-// getIrradianceFromPhtnTree (myObjShader.java:441-458). Exact k nearest within r_max with
-// a shrinking radius; the per-lane max-heap lives in scratch.
+// getIrradianceFromPhtnTree (myObjShader.java:441-458): the k nearest photons with
+// d^2 < max_dist^2 (exact, shrinking radius), summed in the reference's poll order
+// (farthest first) over pi * (largest d^2).
+//
+// Search: the photon BVH (csrc/photon.cpp), nearer child first, a child visited iff
+// its box distance^2 < the current radius^2. The box distance is formed like the
+// photon distance (per-axis differences, squares, same summation order) from bounds
+// no closer than any photon inside, and IEEE rounding is monotonic, so it never
+// exceeds the distance of a photon in the box: no qualifying photon is pruned.
+// The max-heap of (d^2, photon) lives in scratch (one 16-byte entry per slot); it is
+// filled by appending, heapified once when it first holds k entries, and afterwards
+// updated by replacing the root -- the same k-set as push-then-poll.
 static constexpr int KNN_MAX = 256;
+struct KnnE {
+  double d2;
+  int32_t i, pad;
+};
+DEVI void knn_sift_down(KnnE* h, int n, int j) {
+  const KnnE x = h[j];
+  while (true) {
+    int l = 2 * j + 1;
+    if (l >= n) break;
+    int m = l;
+    if (l + 1 < n && h[l + 1].d2 > h[l].d2) m = l + 1;
+    if (!(h[m].d2 > x.d2)) break;
+    h[j] = h[m];
+    j = m;
+  }
+  h[j] = x;
+}
+DEVI double box_d2(const double* mn, const double* mx, const double* p) {
+  double d[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) d[c] = (p[c] < mn[c]) ? (p[c] - mn[c]) : ((p[c] > mx[c]) ? (p[c] - mx[c]) : 0.0);
+  return d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+}
 template <bool CNT>
-DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
-  if (S.photonRoot < 0) return mk(0, 0, 0);
-  double hd[KNN_MAX];
-  int32_t hi[KNN_MAX];
+DEVI V irradiance_heap(const SceneD& S, V p, Counters& ct) {
+  if (S.nphoton == 0) return mk(0, 0, 0);
+  KnnE hp[KNN_MAX];
   int hn = 0;
   const int K = S.photonK < KNN_MAX ? S.photonK : KNN_MAX;
   double maxd2 = S.photonMaxD2;
-  double pos[3] = {p.x, p.y, p.z};
-  int32_t stN[64];
-  uint8_t stS[64];
+  const double pos[3] = {p.x, p.y, p.z};
+  Stack st;  // (box d^2, node<<1 | side) ; the ray-traversal stack is idle during shading
   int sp = 0;
-  stN[0] = S.photonRoot; stS[0] = 0; sp = 1;
-  while (sp > 0) {
-    int32_t ni = stN[sp - 1];
-    const PhotonD& ph = S.photon[ni];
-    uint8_t state = stS[sp - 1];
-    if (state == 0) {
-      if (CNT) ct.c[C_PHOTON]++;
-      stS[sp - 1] = 1;
-      if (ph.axis != -1) {
-        double delta = pos[ph.axis] - ph.pos[ph.axis];
-        int32_t nearC = delta < 0 ? ph.left : ph.right;
-        if (nearC != -1 && sp < 64) { stN[sp] = nearC; stS[sp] = 0; sp++; }
-      }
-      continue;
+  int32_t N = S.photonRoot;
+  while (true) {
+    // N: a node to open
+    const NodeD& nd = S.pnode[N];
+    if (CNT) ct.c[C_PHOTON]++;
+    const double dl = box_d2(nd.lmin, nd.lmax, pos), dr = box_d2(nd.rmin, nd.rmax, pos);
+    const bool vl = dl < maxd2, vr = dr < maxd2;
+    // the nearer child now, the other one pushed (re-checked against the radius when popped)
+    int32_t next = -2;
+    if (vl || vr) {
+      const bool leftFirst = vl && (!vr || dl <= dr);
+      const int side = leftFirst ? 0 : 1;
+      if (vl && vr) { st.setT(sp, leftFirst ? dr : dl); st.setN(sp, (N << 1) | (1 - side)); sp++; }
+      next = (N << 1) | side;
     }
-    if (state == 1) {
-      stS[sp - 1] = 2;
-      if (ph.axis != -1) {
-        double delta = pos[ph.axis] - ph.pos[ph.axis], delta2 = delta * delta;
-        int32_t farC = delta < 0 ? ph.right : ph.left;
-        if (farC != -1 && delta2 < maxd2 && sp < 64) { stN[sp] = farC; stS[sp] = 0; sp++; }
+    while (true) {
+      if (next == -2) {  // pop
+        if (sp == 0) break;
+        --sp;
+        if (!(st.getT(sp) < maxd2)) continue;
+        next = st.getN(sp);
       }
-      continue;
-    }
-    sp--;
-    double dx = pos[0] - ph.pos[0], dy = pos[1] - ph.pos[1], dz = pos[2] - ph.pos[2];
-    double len2 = dx * dx + dy * dy + dz * dz;
-    if (len2 < maxd2) {
-      int i = hn++;  // push into the max-heap
-      hd[i] = len2; hi[i] = ni;
-      while (i > 0) {
-        int par = (i - 1) >> 1;
-        if (hd[par] >= hd[i]) break;
-        double td = hd[par]; hd[par] = hd[i]; hd[i] = td;
-        int32_t ti = hi[par]; hi[par] = hi[i]; hi[i] = ti;
-        i = par;
-      }
-      if (hn > K) {  // poll the most distant
-        hn--;
-        hd[0] = hd[hn]; hi[0] = hi[hn];
-        int j = 0;
-        while (true) {
-          int l = 2 * j + 1, r = l + 1, m = j;
-          if (l < hn && hd[l] > hd[m]) m = l;
-          if (r < hn && hd[r] > hd[m]) m = r;
-          if (m == j) break;
-          double td = hd[m]; hd[m] = hd[j]; hd[j] = td;
-          int32_t ti = hi[m]; hi[m] = hi[j]; hi[j] = ti;
-          j = m;
+      const NodeD& pn = S.pnode[next >> 1];
+      const int side = next & 1;
+      const int32_t child = side ? pn.right : pn.left;
+      if (child >= 0) { N = child; break; }
+      // leaf: scan its photons
+      const int start = side ? pn.pad[2] : pn.pad[0], count = side ? pn.pad[3] : pn.pad[1];
+      if (CNT) ct.c[C_PHOTON] += count;
+      for (int q = 0; q < count; ++q) {
+        const double* ph = S.ppos + 3 * (size_t)(start + q);
+        const double dx = pos[0] - ph[0], dy = pos[1] - ph[1], dz = pos[2] - ph[2];
+        const double len2 = dx * dx + dy * dy + dz * dz;
+        if (len2 < maxd2) {
+          if (hn < K) {
+            hp[hn].d2 = len2; hp[hn].i = start + q;
+            hn++;
+            if (hn == K) {  // heapify once, then the radius is the k-th distance
+              for (int j = K / 2 - 1; j >= 0; --j) knn_sift_down(hp, K, j);
+              if (hp[0].d2 < maxd2) maxd2 = hp[0].d2;
+            }
+          } else {  // len2 < maxd2 = root: replace the farthest
+            hp[0].d2 = len2; hp[0].i = start + q;
+            knn_sift_down(hp, K, 0);
+            if (hp[0].d2 < maxd2) maxd2 = hp[0].d2;
+          }
         }
       }
-      if (hn == K && hd[0] < maxd2) maxd2 = hd[0];
+      next = -2;
+    }
+    if (next == -2 && sp == 0) {
+      // finished (the inner loop broke out at an empty stack)
+      break;
     }
   }
   if (hn == 0) return mk(0, 0, 0);  // [null] -> 0 (Q20)
-  double rSq = hd[0];
-  double area = PI_F * rSq;
+  if (hn < K)
+    for (int j = hn / 2 - 1; j >= 0; --j) knn_sift_down(hp, hn, j);
+  const double rSq = hp[0].d2;
+  const double area = PI_F * rSq;
   V res = mk(0, 0, 0);
-  while (hn > 0) {  // sum in poll order (farthest first), as the reference's near_list
-    const PhotonD& ph = S.photon[hi[0]];
-    res.x += ph.pwr[0]; res.y += ph.pwr[1]; res.z += ph.pwr[2];
+  while (hn > 0) {  // poll order: farthest first
+    const double* w = S.ppwr + 3 * (size_t)hp[0].i;
+    res.x += w[0]; res.y += w[1]; res.z += w[2];
     hn--;
-    hd[0] = hd[hn]; hi[0] = hi[hn];
-    int j = 0;
+    hp[0] = hp[hn];
+    knn_sift_down(hp, hn, 0);
+  }
+  return mk(res.x / area, res.y / area, res.z / area);
+}
+
+// Photon scan: f(d2, photon) for every photon with d2 < R2 (photon BVH, depth first,
+// children pruned by box distance^2 >= R2; see box_d2). Order is irrelevant to its users.
+template <bool CNT, class Fn>
+DEVI void photon_scan(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f) {
+  NStack st;  // the ray-traversal stack is idle during shading
+  int sp = 0;
+  int32_t N = S.photonRoot;
+  while (true) {
+    const NodeD& nd = S.pnode[N];
+    if (CNT) ct.c[C_PHOTON]++;
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const double* mn = side ? nd.rmin : nd.lmin;
+      const double* mx = side ? nd.rmax : nd.lmax;
+      if (!(box_d2(mn, mx, pos) < R2)) continue;
+      const int32_t c = side ? nd.right : nd.left;
+      if (c >= 0) { st.setN(sp++, c); continue; }
+      const int start = side ? nd.pad[2] : nd.pad[0], count = side ? nd.pad[3] : nd.pad[1];
+      if (CNT) ct.c[C_PHOTON] += count;
+      for (int q = 0; q < count; ++q) {
+        const double* ph = S.ppos + 3 * (size_t)(start + q);
+        const double dx = pos[0] - ph[0], dy = pos[1] - ph[1], dz = pos[2] - ph[2];
+        const double d2 = dx * dx + dy * dy + dz * dz;  // myKD_Tree.find_near's distance, same order
+        if (d2 < R2) f(d2, start + q);
+      }
+    }
+    if (sp == 0) break;
+    N = st.getN(--sp);
+  }
+}
+
+// The k nearest photons by selection instead of a heap (no per-lane memory): the
+// k-th smallest d^2 is bracketed by counting passes -- 8 cumulative counters against
+// edges e_1..e_8 of the current window [lo, hi) -- until the window holding the k-th
+// photon has <= KNN_SHELL photons; a last pass sums every photon below the window and
+// the nearest (k - below) window photons (kept sorted in registers). Same k-set and
+// largest d^2 as the heap; the powers are summed in scan order rather than the
+// reference's poll order (a last-ulp difference; DESIGN.md "Precision").
+// Start window: [0, R2) with R2 from the local density of the smallest photon-BVH node
+// around p holding >= k photons; if fewer than k photons fall below it, the next try is
+// that node's far-corner distance (all its photons lie within it), then max_dist^2.
+static constexpr int KNN_SHELL = 8;
+template <bool CNT>
+DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
+#ifdef RT_KNN_HEAP
+  return irradiance_heap<CNT>(S, p, ct);
+#endif
+  if (S.nphoton == 0) return mk(0, 0, 0);
+  const int K = S.photonK;
+  const double R2max = S.photonMaxD2;
+  const double pos[3] = {p.x, p.y, p.z};
+  // --- start bounds from the photon BVH: the smallest node containing p with >= K photons
+  double R2far = R2max, R2dens = R2max;
+  {
+    int32_t N = S.photonRoot;
     while (true) {
-      int l = 2 * j + 1, r = l + 1, m = j;
-      if (l < hn && hd[l] > hd[m]) m = l;
-      if (r < hn && hd[r] > hd[m]) m = r;
-      if (m == j) break;
-      double td = hd[m]; hd[m] = hd[j]; hd[j] = td;
-      int32_t ti = hi[m]; hi[m] = hi[j]; hi[j] = ti;
-      j = m;
+      const NodeD& nd = S.pnode[N];
+      int32_t nxt = -1;
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const int32_t c = side ? nd.right : nd.left;
+        const int cnt = side ? nd.pad[3] : nd.pad[1];
+        const double* mn = side ? nd.rmin : nd.lmin;
+        const double* mx = side ? nd.rmax : nd.lmax;
+        if (c >= 0 && cnt >= K && nxt < 0 && box_d2(mn, mx, pos) == 0.0) nxt = c;
+      }
+      if (nxt < 0) {
+        if (nd.pad[4] >= K) {
+          double mn[3], mx[3], e[3], f[3];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            mn[c] = fmin(nd.lmin[c], nd.rmin[c]); mx[c] = fmax(nd.lmax[c], nd.rmax[c]);
+            e[c] = mx[c] - mn[c];
+            f[c] = fmax(pos[c] - mn[c], mx[c] - pos[c]);  // farthest corner, per axis
+          }
+          // every photon of the node is no farther than the far corner (monotonic rounding)
+          const double far2 = (f[0] * f[0] + f[1] * f[1]) + f[2] * f[2];
+          R2far = fmin(R2max, far2 * (1 + 0x1p-40));
+          // photons lie on surfaces: density over the box's two largest extents
+          const double a = fmax(fmax(e[0] * e[1], e[0] * e[2]), e[1] * e[2]);
+          R2dens = fmin(R2far, 1.3 * K * a / (PI_D * nd.pad[4]));
+        }
+        break;
+      }
+      N = nxt;
     }
   }
+  // --- bracket the k-th d^2: window [lo, hi), `below` photons under lo
+  double lo = 0, hi = R2dens;
+  int below = 0;
+  bool all = false;  // fewer than K photons within max_dist: the set is all of them
+  for (int level = 0; level < 32; ++level) {
+    double e[8];
+    const double w = (hi - lo) * 0.125;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) e[k] = lo + (k + 1) * w;
+    e[7] = hi;
+    uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // photons with d2 < e[k] (including the `below` ones)
+    photon_scan<CNT>(S, pos, hi, ct, [&](double d2, int) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) c[k] += (d2 < e[k]) ? 1u : 0u;
+    });
+    if ((int)c[7] < K) {  // only possible for the start window: widen it
+      if (hi == R2max) { all = true; break; }
+      hi = (hi < R2far) ? R2far : R2max;
+      continue;
+    }
+    int b = 0;
+    while ((int)c[b] < K) ++b;  // first edge with >= K photons below it
+    if (b) { lo = e[b - 1]; below = (int)c[b - 1]; }
+    hi = e[b];
+    if ((int)c[b] - below <= KNN_SHELL || !(lo < hi)) break;
+  }
+  // --- final pass: every photon below the window, and the nearest K - below window photons
+  double sd[KNN_SHELL];
+  int32_t si[KNN_SHELL];
+#pragma unroll
+  for (int k = 0; k < KNN_SHELL; ++k) { sd[k] = DMAX; si[k] = -1; }
+  V res = mk(0, 0, 0);
+  double rSq = 0;
+  int n = 0;
+  photon_scan<CNT>(S, pos, all ? R2max : hi, ct, [&](double d2, int i) {
+    if (all || d2 < lo) {
+      const double* w = S.ppwr + 3 * (size_t)i;
+      res.x += w[0]; res.y += w[1]; res.z += w[2];
+      if (d2 > rSq) rSq = d2;
+      n++;
+    } else {  // window photon: keep the KNN_SHELL nearest, sorted (scan order breaks ties)
+      double xd = d2;
+      int32_t xi = i;
+#pragma unroll
+      for (int k = 0; k < KNN_SHELL; ++k) {
+        if (xd < sd[k]) {
+          const double td = sd[k]; const int32_t ti = si[k];
+          sd[k] = xd; si[k] = xi;
+          xd = td; xi = ti;
+        }
+      }
+    }
+  });
+  if (!all) {
+    const int need = K - below;
+#pragma unroll
+    for (int k = 0; k < KNN_SHELL; ++k)
+      if (k < need && si[k] >= 0) {
+        const double* w = S.ppwr + 3 * (size_t)si[k];
+        res.x += w[0]; res.y += w[1]; res.z += w[2];
+        rSq = sd[k];
+        n++;
+      }
+  }
+  if (n == 0) return mk(0, 0, 0);  // [null] -> 0 (Q20)
+  const double area = PI_F * rSq;
   return mk(res.x / area, res.y / area, res.z / area);
 }
 
@@ -794,7 +975,11 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
   double r = m.ambient[0], g = m.ambient[1], b = m.ambient[2];
   if constexpr ((F & FT_PHOTON) != 0) {
     if (!m.simple && (m.krefl == 0.0) && m.usePhotonMap) {
+#ifdef RT_PROF_NOGATHER  // profiling builds only: results differ
+      V ir = mk(0, 0, 0);
+#else
       V ir = irradiance<CNT>(S, h.fwd, ct);
+#endif
       if (m.isCausticPhtn) { r += ir.x; g += ir.y; b += ir.z; }
       else { r += m.diffuse[0] * ir.x; g += m.diffuse[1] * ir.y; b += m.diffuse[2] * ir.z; }
     }

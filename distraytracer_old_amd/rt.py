@@ -38,7 +38,7 @@ class RenderParams(ctypes.Structure):
 EXPORTS = ["rt_abi_version", "rt_last_error", "rt_device_count", "rt_scene_create", "rt_scene_load_cli",
            "rt_scene_inspect_cli",
            "rt_scene_info", "rt_scene_destroy", "rt_photons_build", "rt_render", "rt_render_device",
-           "rt_render_count", "rt_time_render"]
+           "rt_render_count", "rt_time_render", "rt_scene_photons"]
 
 _lib = None
 
@@ -68,6 +68,8 @@ def lib():
         L.rt_scene_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.rt_scene_destroy.argtypes = [ctypes.c_void_p]
         L.rt_photons_build.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.rt_scene_photons.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                       ctypes.POINTER(ctypes.c_int64)]
         L.rt_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_void_p]
         L.rt_render_count.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p]
@@ -146,6 +148,15 @@ class Scene:
 
     def build_photons(self, seed: int):
         _check(lib().rt_photons_build(self._h, seed), "rt_photons_build")
+
+    def photons(self):
+        """(pos [n,3], pwr [n,3]) of the photon map in photon_list insertion order."""
+        cnt = ctypes.c_int64(0)
+        _check(lib().rt_scene_photons(self._h, None, None, 0, ctypes.byref(cnt)), "rt_scene_photons")
+        n = cnt.value
+        pos = np.zeros((n, 3)); pwr = np.zeros((n, 3))
+        _check(lib().rt_scene_photons(self._h, pos.ctypes.data, pwr.ctypes.data, n, ctypes.byref(cnt)), "rt_scene_photons")
+        return pos, pwr
 
     def render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, flags=0):
         p = params(W, H, spp, seed, rows, row_step, flags)

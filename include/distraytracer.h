@@ -172,6 +172,10 @@ void rt_scene_destroy(rt_scene* scene);
 
 /* photon-map pre-pass (myScene.initRender :1096-1099); idempotent per scene */
 int rt_photons_build(rt_scene* scene, uint64_t seed);
+/* The photon map built by rt_photons_build as the reference's photon_list (myScene.java:1000-1091,
+   insertion order): *count = number of photons; copies min(n, count) positions / powers
+   (double[3] each) to pos / pwr. */
+int rt_scene_photons(const rt_scene* scene, double* pos, double* pwr, int64_t n, int64_t* count);
 
 /* Blocking render into caller-owned HOST buffers (either may be NULL).
    rgb: float[n_rows*width*3] clamped <=1 per myColor; argb: int32[n_rows*width], reference packing. */

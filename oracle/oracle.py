@@ -45,6 +45,7 @@ def lib():
         L.oracle_free.argtypes = [ctypes.c_void_p]
         L.oracle_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_build_photons.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.oracle_photons.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_int]
@@ -72,6 +73,13 @@ class OracleScene:
 
     def build_photons(self, seed: int) -> int:
         return lib().oracle_build_photons(self._h, seed)
+
+    def photons(self):
+        """(pos [n,3], pwr [n,3]) of the photon map in insertion order (after build_photons)."""
+        n = lib().oracle_photons(self._h, None, None, 0)
+        pos = np.zeros((n, 3)); pwr = np.zeros((n, 3))
+        lib().oracle_photons(self._h, pos.ctypes.data, pwr.ctypes.data, n)
+        return pos, pwr
 
     def render(self, W: int, H: int, spp: int = 0, seed: int = 0x5EED0001, rows=None, row_step: int = 1,
                threads: int = 0):

@@ -1895,6 +1895,15 @@ int oracle_build_photons(void* p, uint64_t seed) {
   return (int)s->photonTree.photons.size();
 }
 
+// photon_list in insertion order (test access): pos/pwr = double[n*3]; returns the count
+int oracle_photons(void* p, double* pos, double* pwr, int n) {
+  Scene* s = (Scene*)p;
+  const std::vector<Photon>& ph = s->photonTree.photons;
+  for (int i = 0; i < n && i < (int)ph.size(); ++i)
+    for (int c = 0; c < 3; ++c) { pos[3 * i + c] = ph[i].pos[c]; pwr[3 * i + c] = ph[i].pwr[c]; }
+  return (int)ph.size();
+}
+
 // Render rows [row0,row1) with stride rowStep of a W x H image (myFOVScene.draw,
 // myScene.java:1481-1531 + DOF :1386-1443). spp<=0 keeps the scene's
 // rays_per_pixel. rgb: float[nrows*W*3], argb: int32[nrows*W]; stats: uint64[16].

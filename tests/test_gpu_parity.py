@@ -109,6 +109,14 @@ def test_photon_map_parity(tmp_path, mode, spec):
     g.build_photons(seed)
     n_o = o.build_photons(seed)
     assert g.info()["photons"] == n_o
+    # the photon_list itself, in insertion order: emission directions go through sin/cos/acos,
+    # whose device and host libm differ in last bits, so positions agree to rounding level
+    # except where such a difference flips a discrete decision of a photon path
+    gp, gw = g.photons()
+    op, ow = o.photons()
+    far = np.abs(gp - op).max(axis=1) > 1e-9
+    assert far.mean() < 2e-3, far.mean()
+    assert np.array_equal(gw[~far], ow[~far])
     rg, ag = g.render(64, 64, spp=2, seed=seed)
     ro, ao, _ = o.render(64, 64, spp=2, seed=seed)
     c = compare(rg, ag, ro, ao)
@@ -116,7 +124,8 @@ def test_photon_map_parity(tmp_path, mode, spec):
 
 
 @pytest.mark.parametrize("cli,W,spp", [("c3_bun69k.cli", 128, 2), ("t01.cli", 128, 1), ("p2_t05.cli", 96, 2),
-                                       ("c2clear.cli", 96, 1), ("plnts3ColsBunnies.cli", 96, 1)])
+                                       ("c2clear.cli", 96, 1), ("plnts3ColsBunnies.cli", 96, 1),
+                                       ("t11.cli", 64, 1)])
 def test_specialised_kernel_equals_generic(cli, W, spp):
     """The feature-specialised kernel variant picked for a scene renders bit-identically
     to the all-features kernel (RT_RENDER_GENERIC)."""

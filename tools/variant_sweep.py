@@ -23,6 +23,8 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "noshadow": ["RT_PROF_NOSHADOW"],          # profiling only: results differ
     "nosec": ["RT_PROF_NOSECONDARY"],
     "primary": ["RT_PROF_NOSHADOW", "RT_PROF_NOSECONDARY"],
+    "nogather": ["RT_PROF_NOGATHER"],
+    "knnheap": ["RT_KNN_HEAP"],
 }
 FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS"}
 
