@@ -137,6 +137,7 @@ struct Stack {
     else sN[i - STK_LDS] = v;
   }
 };
+
 struct NStack {  // shadow traversal: node indices only
   int32_t sN[BVH_STACK - STK_LDS];
   DEVI int32_t getN(int i) const {
@@ -1131,13 +1132,13 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
 #endif
 static constexpr int XCD_CHUNKS = RT_XCD_CHUNKS;
 __host__ __device__ inline int xcd_grid(int ntiles) {
-  if (XCD_CHUNKS == 0) return ntiles;
-  const int nch = 8 * XCD_CHUNKS, csz = (ntiles + nch - 1) / nch;
+  if constexpr (XCD_CHUNKS == 0) return ntiles;
+  const int nch = 8 * (XCD_CHUNKS ? XCD_CHUNKS : 1), csz = (ntiles + nch - 1) / nch;
   return nch * csz;
 }
 DEVI int tile_of_block(int b, int ntiles) {
-  if (XCD_CHUNKS == 0) return b;
-  const int nch = 8 * XCD_CHUNKS, csz = (ntiles + nch - 1) / nch;
+  if constexpr (XCD_CHUNKS == 0) return b;
+  const int nch = 8 * (XCD_CHUNKS ? XCD_CHUNKS : 1), csz = (ntiles + nch - 1) / nch;
   const int xcd = b & 7, slot = b >> 3;
   const int t = ((slot / csz) * 8 + xcd) * csz + slot % csz;
   return t < ntiles ? t : -1;
