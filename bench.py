@@ -62,8 +62,11 @@ def traced_rays(st: dict) -> int:
 
 
 def find_traffic(workload: str):
-    """Per-launch HBM bytes from the newest committed PMC summary for this workload."""
+    """Per-launch HBM bytes from the newest committed PMC summary for this workload
+    (profiles/rNN_*pmc*.json; BENCH_TRAFFIC_JSON names one explicitly)."""
     files = sorted(glob.glob(str(REPO / "profiles" / "*pmc*.json")))
+    if os.environ.get("BENCH_TRAFFIC_JSON"):
+        files = [os.environ["BENCH_TRAFFIC_JSON"]]
     for f in reversed(files):
         try:
             d = json.loads(Path(f).read_text())

@@ -195,7 +195,10 @@ static int make_params(rt_scene* s, const rt_render_params* p, ParamsD& P) {
   P.seed = p->seed;
   // wave layout (render_kernel): G = largest power of two <= min(spp, 64) sample lanes per pixel
   int G = 1;
-  while (G * 2 <= P.spp && G * 2 <= 64) G *= 2;
+#ifndef RT_MAX_G
+#define RT_MAX_G 64
+#endif
+  while (G * 2 <= P.spp && G * 2 <= RT_MAX_G) G *= 2;
   static const int TW[7] = {8, 8, 4, 4, 2, 2, 1};  // pixels per wave 64, 32, ..., 1 as tw x th
   int lg = 0;
   while ((1 << lg) < G) ++lg;

@@ -868,6 +868,9 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
       g += tex.y * L.color[1] * ldp;
       b += tex.z * L.color[2] * ldp;
     }
+#ifdef RT_PROF_NOPHONG  // profiling builds only: results differ
+    continue;
+#endif
     if (m.phong == 0) continue;
     V hN = nrmz(mk(sr.d.x - h.dw.x, sr.d.y - h.dw.y, sr.d.z - h.dw.z));
     double hdp = dot(hN, h.nrm) * ltMult;

@@ -1,16 +1,19 @@
 #!/bin/bash
-# One GPU session: smoke -> bench (N=1) -> rocprofv3 kernel trace -> rocprofv3 FETCH_SIZE pass.
+# One GPU evidence session: smoke -> rocprofv3 kernel trace -> rocprofv3 FETCH_SIZE pass ->
+# PMC summary -> bench (N=1, with that summary as its traffic source) -> pytest -m gpu.
 # Every GPU step has its own time limit; steps are chained with && so a failure stops the chain.
 set -o pipefail
 TAG=${1:-r01}
 OUT=gpurun_out/$TAG
+WL="C3 c3_bun69k.cli 1024x1024 16spp"
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
-timeout -k 10 600 python3 bench.py --steps 10 --warmup 2 > $OUT/bench.json 2> $OUT/bench.err && \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1 && \
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > $OUT/pmc.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof.log 2>&1 && \
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > $OUT/pmc.log 2>&1 && \
+python3 tools/pmc_summary.py $OUT/prof/run_kernel_stats.csv $OUT/pmc/run_counter_collection.csv "$WL" $OUT/c3_pmc.json > $OUT/pmc_summary.log 2>&1 && \
+BENCH_TRAFFIC_JSON=$OUT/c3_pmc.json timeout -k 10 600 python3 bench.py --steps 20 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err && \
+timeout -k 10 600 python3 -m pytest tests -m gpu -q > $OUT/pytest_gpu.log 2>&1
 rc=$?
 echo "chain exit $rc" >> $OUT/status.txt
-find $OUT -name "*.csv" | head -20 >> $OUT/status.txt
 exit $rc

@@ -25,8 +25,9 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "primary": ["RT_PROF_NOSHADOW", "RT_PROF_NOSECONDARY"],
     "nogather": ["RT_PROF_NOGATHER"],
     "knnheap": ["RT_KNN_HEAP"],
+    "nophong": ["RT_PROF_NOPHONG"],
 }
-FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS"}
+FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS", "g": "RT_MAX_G"}
 
 
 def defines_of(name: str) -> list[str]:
