@@ -132,6 +132,10 @@ def main():
 
     tex = scenes.prepare(cli)
     scene = rt.Scene.load_cli(cli, textures=tex, device=local)
+    info = scene.info()
+    if info["photon_mode"]:  # photon pre-pass (initRender), outside the timed region; sharded over ranks
+        from distraytracer_old_amd import multigpu as _mg
+        _mg.build_photons_sharded(scene, seed, info["photon_count"], dist)
     # this rank's rows: r, r+N, ...
     p = rt.params(W, H, spp=spp, seed=seed, rows=(rank, H), row_step=world)
     nrows = rt.nrows_of(p)
@@ -203,8 +207,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: bun69k = deterministic subdivision of data/bun500.cli (69,451 tris); "
-                    "scene data/p3_t09.cli without the wood line",
+            "data": ("synthetic: bun69k = deterministic subdivision of data/bun500.cli (69,451 tris); "
+                     "scene data/p3_t09.cli without the wood line") if args.config == "C3" else
+                    f"scene scenes/{cli} (SURVEY 8(d) {args.config}); synthetic inputs where the reference's are missing",
             "config": {"workload": workload, "width": W, "height": H, "spp": spp, "seed": seed,
                        "rays_per_frame": int(rays_frame), "camera_samples": int(cam_frame),
                        "parallelism": f"rows interleaved over {world} rank(s)" +

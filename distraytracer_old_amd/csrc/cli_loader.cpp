@@ -422,8 +422,9 @@ extern "C" int rt_scene_inspect_cli(const char* scene_dir, const char* cli_file,
                             hs.node.size() * sizeof(NodeD) + hs.leaf.size() * sizeof(LeafD) + hs.member.size() * 4 +
                             hs.accel.size() * sizeof(AccelD) + hs.top.size() * sizeof(TopD) + hs.mat.size() * sizeof(MatD) +
                             hs.light.size() * sizeof(LightD) + hs.texel.size() * 4);
-  int64_t v[12] = {(int64_t)hs.top.size(), (int64_t)hs.light.size(), hs.bvhInternal, hs.bvhLeaves, hs.bvhDepth,
-                   hs.bvhPrims, hs.nprims, hs.rpp, bytes, (int64_t)hs.tri.size(), 0, (int64_t)hs.mat.size()};
-  for (int i = 0; i < n && i < 12; ++i) info[i] = v[i];
+  int64_t v[14] = {(int64_t)hs.top.size(), (int64_t)hs.light.size(), hs.bvhInternal, hs.bvhLeaves, hs.bvhDepth,
+                   hs.bvhPrims, hs.nprims, hs.rpp, bytes, (int64_t)hs.tri.size(), 0, (int64_t)hs.mat.size(),
+                   hs.photonMode, hs.photonCount};
+  for (int i = 0; i < n && i < 14; ++i) info[i] = v[i];
   return RT_OK;
 }

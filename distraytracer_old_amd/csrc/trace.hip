@@ -148,10 +148,10 @@ int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
 int rt_scene_info(const rt_scene* s, int64_t* info, int n) {
   if (!s || !info) return set_error(RT_E_INVALID, "null argument");
   const HostScene& h = s->hs;
-  int64_t v[12] = {(int64_t)h.top.size(), (int64_t)h.light.size(), h.bvhInternal, h.bvhLeaves, h.bvhDepth,
+  int64_t v[14] = {(int64_t)h.top.size(), (int64_t)h.light.size(), h.bvhInternal, h.bvhLeaves, h.bvhDepth,
                    h.bvhPrims, h.nprims, h.rpp, (int64_t)s->devBytes, (int64_t)h.tri.size(),
-                   (int64_t)h.nphoton, (int64_t)h.mat.size()};
-  for (int i = 0; i < n && i < 12; ++i) info[i] = v[i];
+                   (int64_t)h.nphoton, (int64_t)h.mat.size(), h.photonMode, h.photonCount};
+  for (int i = 0; i < n && i < 14; ++i) info[i] = v[i];
   return RT_OK;
 }
 
@@ -351,44 +351,97 @@ int rt_time_render(rt_scene* s, const rt_render_params* p, int warmup, int iters
 }  // extern "C"
 
 int rt_upload_photons(rt_scene* s);
+
+// Shoot photons [first, first+count) of every light (myScene.sendCausticPhotons :952-998 /
+// sendDiffusePhotons :1000-1091 with the emitted-photon index range restricted) into
+// pos/pwr in photon_list order: light, photon index, path slot. Chunked so the
+// per-lane slot buffers stay bounded for any photon count.
+static int shoot_photons(rt_scene* s, uint64_t seed, int64_t first, int64_t count, std::vector<double>& pos,
+                         std::vector<double>& pwr, std::vector<int64_t>& perLight) {
+  HostScene& h = s->hs;
+  pos.clear();
+  pwr.clear();
+  perLight.assign(h.light.size(), 0);
+  const long total = (long)h.light.size() * count;
+  if (total <= 0) return RT_OK;
+  HIPCHK(hipSetDevice(s->device));
+  const long CH = std::min<long>(total, 1L << 22);
+  dv::PhotonOut* d_out = nullptr;
+  int* d_cnt = nullptr;
+  HIPCHK(hipMalloc(&d_out, sizeof(dv::PhotonOut) * dv::PH_SLOTS * CH));
+  hipError_t e = hipMalloc(&d_cnt, sizeof(int) * CH);
+  const bool caustic = h.photonMode == 2;
+  const double pwrMult = (caustic ? 40.0 : 8.0) / h.photonCount;  // causticsLightPwrMult / diffuseLightPwrMult (myScene.java:109-110)
+  std::vector<int> cnt(CH);
+  std::vector<dv::PhotonOut> out((size_t)dv::PH_SLOTS * CH);
+  for (long base = 0; base < total && e == hipSuccess; base += CH) {
+    const long n = std::min(CH, total - base);
+    hipLaunchKernelGGL(dv::photon_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), dv::LDS_BYTES, 0, s->dev, seed,
+                       (long)first, (long)count, base, n, caustic ? 1 : 0, pwrMult, d_out, d_cnt);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(cnt.data(), d_cnt, sizeof(int) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out.data(), d_out, sizeof(dv::PhotonOut) * dv::PH_SLOTS * n, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) break;
+    for (long g = 0; g < n; ++g)
+      for (int j = 0; j < cnt[g]; ++j) {
+        const dv::PhotonOut& p = out[(size_t)g * dv::PH_SLOTS + j];
+        pos.insert(pos.end(), p.pos, p.pos + 3);
+        pwr.insert(pwr.end(), p.pwr, p.pwr + 3);
+        perLight[(base + g) / count]++;
+      }
+  }
+  (void)hipFree(d_out);
+  (void)hipFree(d_cnt);
+  if (e != hipSuccess) return set_error(RT_E_HIP, std::string("photon pre-pass: ") + hipGetErrorString(e));
+  return RT_OK;
+}
+
+static int check_photon_params(const HostScene& h) {
+  if (h.photonMode == 0) return set_error(RT_E_INVALID, "scene has no photon map");
+  if (h.photonCount <= 0 || h.photonK <= 0) return set_error(RT_E_INVALID, "bad photon parameters");
+  if (h.photonK > dv::KNN_MAX) return set_error(RT_E_INVALID, "photon neighbourhood k > 256 unsupported");
+  return RT_OK;
+}
+
 extern "C" int rt_photons_build(rt_scene* s, uint64_t seed) {
   if (!s) return set_error(RT_E_INVALID, "null scene");
   HostScene& h = s->hs;
   if (h.photonMode == 0 || s->photonsUploaded) return RT_OK;
-  if (h.photonCount <= 0 || h.photonK <= 0) return set_error(RT_E_INVALID, "bad photon parameters");
-  if (h.photonK > dv::KNN_MAX) return set_error(RT_E_INVALID, "photon neighbourhood k > 256 unsupported");
-  HIPCHK(hipSetDevice(s->device));
-  const long total = (long)h.light.size() * h.photonCount;
-  std::vector<int> cnt(total > 0 ? total : 1);
-  std::vector<dv::PhotonOut> out;
-  if (total > 0) {
-    dv::PhotonOut* d_out = nullptr;
-    int* d_cnt = nullptr;
-    HIPCHK(hipMalloc(&d_out, sizeof(dv::PhotonOut) * dv::PH_SLOTS * total));
-    HIPCHK(hipMalloc(&d_cnt, sizeof(int) * total));
-    bool caustic = h.photonMode == 2;
-    double pwrMult = (caustic ? 40.0 : 8.0) / h.photonCount;  // causticsLightPwrMult / diffuseLightPwrMult (myScene.java:109-110)
-    long blocks = (total + 63) / 64;
-    hipLaunchKernelGGL(dv::photon_kernel, dim3((unsigned)blocks), dim3(64), dv::LDS_BYTES, 0, s->dev, seed, h.photonCount, caustic ? 1 : 0,
-                       pwrMult, d_out, d_cnt);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(cnt.data(), d_cnt, sizeof(int) * total, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) {
-      out.resize((size_t)dv::PH_SLOTS * total);
-      e = hipMemcpy(out.data(), d_out, sizeof(dv::PhotonOut) * dv::PH_SLOTS * total, hipMemcpyDeviceToHost);
-    }
-    (void)hipFree(d_out);
-    (void)hipFree(d_cnt);
-    if (e != hipSuccess) return set_error(RT_E_HIP, std::string("photon pre-pass: ") + hipGetErrorString(e));
-  }
+  int rc = check_photon_params(h);
+  if (rc) return rc;
   std::vector<double> pos, pwr;
-  for (long g = 0; g < total; ++g)
-    for (int j = 0; j < cnt[g]; ++j) {
-      const dv::PhotonOut& p = out[(size_t)g * dv::PH_SLOTS + j];
-      pos.insert(pos.end(), p.pos, p.pos + 3);
-      pwr.insert(pwr.end(), p.pwr, p.pwr + 3);
-    }
+  std::vector<int64_t> perLight;
+  if ((rc = shoot_photons(s, seed, 0, h.photonCount, pos, pwr, perLight))) return rc;
   build_photon_tree(h, pos, pwr);
+  return rt_upload_photons(s);
+}
+
+extern "C" int rt_photons_shoot(rt_scene* s, uint64_t seed, int64_t first, int64_t count, int64_t* per_light) {
+  if (!s) return set_error(RT_E_INVALID, "null scene");
+  HostScene& h = s->hs;
+  int rc = check_photon_params(h);
+  if (rc) return rc;
+  if (first < 0 || count < 0 || first + count > h.photonCount) return set_error(RT_E_INVALID, "photon range out of bounds");
+  std::vector<double> pos, pwr;
+  std::vector<int64_t> perLight;
+  if ((rc = shoot_photons(s, seed, first, count, pos, pwr, perLight))) return rc;
+  h.photonListPos.swap(pos);
+  h.photonListPwr.swap(pwr);
+  h.nphoton = (int64_t)(h.photonListPos.size() / 3);
+  if (per_light)
+    for (size_t l = 0; l < perLight.size(); ++l) per_light[l] = perLight[l];
+  return RT_OK;
+}
+
+extern "C" int rt_photons_set(rt_scene* s, const double* pos, const double* pwr, int64_t n) {
+  if (!s || n < 0 || (n > 0 && (!pos || !pwr))) return set_error(RT_E_INVALID, "bad photon list");
+  HostScene& h = s->hs;
+  int rc = check_photon_params(h);
+  if (rc) return rc;
+  if (n > INT32_MAX / 4) return set_error(RT_E_INVALID, "photon map too large");
+  std::vector<double> p(pos, pos + 3 * n), w(pwr, pwr + 3 * n);
+  build_photon_tree(h, p, w);
+  s->photonsUploaded = false;
   return rt_upload_photons(s);
 }

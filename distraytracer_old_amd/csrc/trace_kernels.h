@@ -1339,13 +1339,17 @@ DEVI void new_wray(WRay& w, V o, V d) {
   w.o = o; w.d = nrmz(d); w.d0 = w.d; w.stable = false; w.moved = false; w.ver = 0;
 }
 
-__global__ void __launch_bounds__(64) photon_kernel(SceneD S, uint64_t seed, int numCast, int caustic, double pwrMult,
+// Lane gid of a launch covers photon (light li, index i) of the shard [first, first+count)
+// of every light, light-major: g = gBase + gid, li = g / count, i = first + g % count.
+__global__ void __launch_bounds__(64) photon_kernel(SceneD S, uint64_t seed, long first, long count, long gBase,
+                                                   long nLanes, int caustic, double pwrMult,
                                                    PhotonOut* __restrict__ out, int* __restrict__ cnt) {
   constexpr uint32_t F = FT_ALL;
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (long)S.nlight * numCast) return;
-  const int li = (int)(gid / numCast);
-  const uint64_t i = (uint64_t)(gid % numCast);
+  if (gid >= nLanes) return;
+  const long g = gBase + gid;
+  const int li = (int)(g / count);
+  const uint64_t i = (uint64_t)(first + g % count);
   const LightD& L = S.light[li];
   Counters ct;
   int n = 0;

@@ -40,3 +40,45 @@ def gather_tiles(tile, dist, group=None):
     out = torch.empty((world,) + tuple(tile.shape), dtype=tile.dtype, device=tile.device)
     dist.all_gather_into_tensor(out.view(-1), tile.contiguous().view(-1), group=group)
     return out
+
+
+def photon_shard(rank: int, world: int, count: int) -> tuple[int, int]:
+    """Emitted-photon index range [first, first+n) of a rank (every light)."""
+    first = rank * count // world
+    return first, (rank + 1) * count // world - first
+
+
+def merge_photon_shards(shards):
+    """shards: per rank (pos [n,3], pwr [n,3], per_light [L]) in rank order -> the full
+    photon_list in the reference's insertion order: light-major, then photon index
+    (rank shards hold consecutive index ranges), then path order."""
+    import numpy as np
+
+    pos, pwr = [], []
+    nl = len(shards[0][2])
+    offs = [np.concatenate([[0], np.cumsum(s[2])]) for s in shards]
+    for light in range(nl):
+        for r, (p, w, _) in enumerate(shards):
+            a, b = offs[r][light], offs[r][light + 1]
+            pos.append(p[a:b]); pwr.append(w[a:b])
+    return np.concatenate(pos), np.concatenate(pwr)
+
+
+def build_photons_sharded(scene, seed: int, count: int, dist=None):
+    """The photon pre-pass split over ranks: each rank shoots its index range,
+    the shards are all-gathered, every rank builds the same photon map."""
+    import numpy as np
+
+    rank = dist.get_rank() if dist else 0
+    world = dist.get_world_size() if dist else 1
+    first, n = photon_shard(rank, world, count)
+    pos, pwr, per = scene.shoot_photons(seed, first, n)
+    if dist is None:
+        shards = [(pos, pwr, per)]
+    else:
+        objs = [None] * world
+        dist.all_gather_object(objs, (pos, pwr, per))
+        shards = objs
+    full_pos, full_pwr = merge_photon_shards(shards)
+    scene.set_photons(full_pos, full_pwr)
+    return len(full_pos)

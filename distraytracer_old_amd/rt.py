@@ -18,7 +18,8 @@ from .scenes import SCENE_DIR, prepare
 ST_NAMES = ["camera", "shadow", "refl", "refr", "box", "tri", "quad", "implicit", "light", "photon", "texel",
             "node", "leaf", "member", "root", "top"]
 INFO_NAMES = ["objects", "lights", "bvh_internal", "bvh_leaves", "bvh_depth", "bvh_prims", "prims",
-              "rays_per_pixel", "device_bytes", "triangles", "photons", "materials"]
+              "rays_per_pixel", "device_bytes", "triangles", "photons", "materials", "photon_mode",
+              "photon_count"]
 
 
 class RTError(RuntimeError):
@@ -38,7 +39,7 @@ class RenderParams(ctypes.Structure):
 EXPORTS = ["rt_abi_version", "rt_last_error", "rt_device_count", "rt_scene_create", "rt_scene_load_cli",
            "rt_scene_inspect_cli",
            "rt_scene_info", "rt_scene_destroy", "rt_photons_build", "rt_render", "rt_render_device",
-           "rt_render_count", "rt_time_render", "rt_scene_photons"]
+           "rt_render_count", "rt_time_render", "rt_scene_photons", "rt_photons_shoot", "rt_photons_set"]
 
 _lib = None
 
@@ -70,6 +71,8 @@ def lib():
         L.rt_photons_build.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         L.rt_scene_photons.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                        ctypes.POINTER(ctypes.c_int64)]
+        L.rt_photons_shoot.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+        L.rt_photons_set.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         L.rt_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_void_p]
         L.rt_render_count.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p]
@@ -105,9 +108,9 @@ def inspect_cli(cli: str, scene_dir=SCENE_DIR, textures: dict | None = None) -> 
     if textures is None:
         textures = prepare(cli, Path(scene_dir))
     names, arrs, cnames, tds = _tex_args(textures)
-    v = np.zeros(12, dtype=np.int64)
+    v = np.zeros(len(INFO_NAMES), dtype=np.int64)
     _check(lib().rt_scene_inspect_cli(str(scene_dir).encode(), cli.encode(), len(names), cnames, tds,
-                                      v.ctypes.data, 12), "rt_scene_inspect_cli")
+                                      v.ctypes.data, len(INFO_NAMES)), "rt_scene_inspect_cli")
     return dict(zip(INFO_NAMES, v.tolist()))
 
 
@@ -142,12 +145,25 @@ class Scene:
         return cls(h)
 
     def info(self) -> dict:
-        v = np.zeros(12, dtype=np.int64)
-        _check(lib().rt_scene_info(self._h, v.ctypes.data, 12), "rt_scene_info")
+        v = np.zeros(len(INFO_NAMES), dtype=np.int64)
+        _check(lib().rt_scene_info(self._h, v.ctypes.data, len(INFO_NAMES)), "rt_scene_info")
         return dict(zip(INFO_NAMES, v.tolist()))
 
     def build_photons(self, seed: int):
         _check(lib().rt_photons_build(self._h, seed), "rt_photons_build")
+
+    def shoot_photons(self, seed: int, first: int, count: int):
+        """Photon shard [first, first+count) of every light -> (pos, pwr, per_light counts)."""
+        nl = self.info()["lights"]
+        per = np.zeros(max(1, nl), dtype=np.int64)
+        _check(lib().rt_photons_shoot(self._h, seed, first, count, per.ctypes.data), "rt_photons_shoot")
+        pos, pwr = self.photons()
+        return pos, pwr, per[:nl]
+
+    def set_photons(self, pos, pwr):
+        pos = np.ascontiguousarray(pos, dtype=np.float64)
+        pwr = np.ascontiguousarray(pwr, dtype=np.float64)
+        _check(lib().rt_photons_set(self._h, pos.ctypes.data, pwr.ctypes.data, len(pos)), "rt_photons_set")
 
     def photons(self):
         """(pos [n,3], pwr [n,3]) of the photon map in photon_list insertion order."""

@@ -165,8 +165,9 @@ int rt_scene_load_cli(const char* scene_dir, const char* cli_file, int num_textu
 /* Host-only parse + build (no device): fills the rt_scene_info fields; device bytes = layout bytes. */
 int rt_scene_inspect_cli(const char* scene_dir, const char* cli_file, int num_textures, const char* const* texture_names,
                          const rt_texture_desc* textures, int64_t* info, int n);
-/* info[0..11]: objects, lights, bvh_internal, bvh_leaves, bvh_depth, bvh_prims, prims, rays_per_pixel,
-   device bytes, triangles, photons, materials */
+/* info[0..13]: objects, lights, bvh_internal, bvh_leaves, bvh_depth, bvh_prims, prims, rays_per_pixel,
+   device bytes, triangles, photons (stored), materials, photon mode (0 none / 1 diffuse / 2 caustic),
+   photons emitted per light */
 int rt_scene_info(const rt_scene* scene, int64_t* info, int n);
 void rt_scene_destroy(rt_scene* scene);
 
@@ -176,6 +177,13 @@ int rt_photons_build(rt_scene* scene, uint64_t seed);
    insertion order): *count = number of photons; copies min(n, count) positions / powers
    (double[3] each) to pos / pwr. */
 int rt_scene_photons(const rt_scene* scene, double* pos, double* pwr, int64_t n, int64_t* count);
+/* Sharded pre-pass (multi-GPU): shoot only emitted photons [first, first+count) of
+   every light (same keyed RNG, so the union of shards is the full pre-pass); the scene's
+   photon_list becomes that shard (light-major, then photon index, then path order) without a
+   search structure; per_light[num_lights] (may be NULL) receives the shard's count per light. */
+int rt_photons_shoot(rt_scene* scene, uint64_t seed, int64_t first, int64_t count, int64_t* per_light);
+/* Set the photon_list (insertion order) and build / upload the photon map from it. */
+int rt_photons_set(rt_scene* scene, const double* pos, const double* pwr, int64_t n);
 
 /* Blocking render into caller-owned HOST buffers (either may be NULL).
    rgb: float[n_rows*width*3] clamped <=1 per myColor; argb: int32[n_rows*width], reference packing. */

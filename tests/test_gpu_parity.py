@@ -134,3 +134,27 @@ def test_specialised_kernel_equals_generic(cli, W, spp):
     rg, ag = g.render(W, W, spp=spp, seed=SEED, flags=rt.RENDER_GENERIC)
     assert np.array_equal(as_, ag)
     assert np.array_equal(rs.view(np.uint32), rg.view(np.uint32))
+
+
+def test_photon_shards_merge_to_the_full_prepass(tmp_path):
+    """Multi-GPU photon pre-pass (8(e)): shards shot separately and merged in rank order give
+    the single-GPU photon_list bit for bit, and the same image."""
+    from distraytracer_old_amd import multigpu
+    src = (scenes.SCENE_DIR / "t11.cli").read_text().replace("diffuse_photons  1000000  200 0.1",
+                                                             "diffuse_photons  30001  50 0.1")
+    (tmp_path / "t11s.cli").write_text(src)
+    seed = 0x5EED0005
+    full = rt.Scene.load_cli("t11s.cli", scene_dir=tmp_path, textures={})
+    full.build_photons(seed)
+    fp, fw = full.photons()
+    sh = rt.Scene.load_cli("t11s.cli", scene_dir=tmp_path, textures={})
+    shards = []
+    for r in range(3):
+        first, n = multigpu.photon_shard(r, 3, 30001)
+        shards.append(sh.shoot_photons(seed, first, n))
+    mp, mw = multigpu.merge_photon_shards(shards)
+    assert np.array_equal(mp, fp) and np.array_equal(mw, fw)
+    sh.set_photons(mp, mw)
+    a = full.render(64, 64, spp=2, seed=seed)
+    b = sh.render(64, 64, spp=2, seed=seed)
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0])

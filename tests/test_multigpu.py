@@ -72,3 +72,26 @@ def test_assemble_numpy_ragged():
         tiles[r, : rows.shape[0]] = rows
         assert rows.shape[0] == multigpu.tile_rows(r, world, H)
     assert np.array_equal(multigpu.assemble(tiles, H), img)
+
+
+def test_merge_photon_shards_restores_insertion_order():
+    """Shards (rank r holds emitted-photon indices [r*P/N, (r+1)*P/N) of every light, each
+    light-major) merge back into the reference's light-major photon_list order."""
+    import numpy as np
+    from distraytracer_old_amd import multigpu
+
+    # full list: light 0 photons 0..9 (some store 0 or 2 photons), light 1 photons 0..9
+    rng = np.random.default_rng(1)
+    stored = rng.integers(0, 3, size=(2, 10))
+    full = [(l, i, k) for l in range(2) for i in range(10) for k in range(stored[l, i])]
+    pos_full = np.array([[l, i, k] for l, i, k in full], dtype=float)
+    shards = []
+    for r in range(3):
+        first, n = multigpu.photon_shard(r, 3, 10)
+        rows = [(l, i, k) for l in range(2) for i in range(first, first + n) for k in range(stored[l, i])]
+        per = np.array([sum(1 for x in rows if x[0] == l) for l in range(2)])
+        p = np.array([[l, i, k] for l, i, k in rows], dtype=float).reshape(-1, 3)
+        shards.append((p, p * 2, per))
+    mp, mw = multigpu.merge_photon_shards(shards)
+    assert np.array_equal(mp, pos_full) and np.array_equal(mw, pos_full * 2)
+    assert sum(multigpu.photon_shard(r, 3, 10)[1] for r in range(3)) == 10
