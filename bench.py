@@ -5,8 +5,8 @@ metric  "Mray/s + achieved HBM GB/s, bun69k.cli 1024^2 16spp, 1/2/4/8 GPU"
 workload C3 = scenes/c3_bun69k.cli (data/p3_t09.cli without `wood`) with the
          synthetic bun69k (69,451 triangles), 1024x1024, 16 spp, seed 0x5EED0001.
 
-One step = one full C3 frame: every rank renders its rows (rank r renders rows
-r, r+N, r+2N, ... -- interleaved for load balance) with the HIP kernel into a
+One step = one full C3 frame: every rank renders its rows (rank r renders the
+8-row bands r, r+N, r+2N, ... -- interleaved for load balance) with the HIP kernel into a
 device buffer, then (N>1) the per-rank float-RGB tiles are gathered to rank 0
 over RCCL (`all_gather_into_tensor`). Work per step is one frame whatever N is
 (strong scaling). value = traced rays of the frame (camera + shadow + reflection
@@ -137,12 +137,14 @@ def main():
         from distraytracer_old_amd import multigpu as _mg
         _mg.build_photons_sharded(scene, seed, info["photon_count"], dist)
     # this rank's rows: r, r+N, ...
-    p = rt.params(W, H, spp=spp, seed=seed, rows=(rank, H), row_step=world)
+    from distraytracer_old_amd import multigpu
+    r0, r1, step, band = multigpu.rows_of(rank, world, H)
+    p = rt.params(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=step, row_band=band)
     nrows = rt.nrows_of(p)
-    maxrows = (H + world - 1) // world
+    maxrows = multigpu.max_tile_rows(world, H)
 
     # exact per-frame counters (instrumented run, outside the timed region)
-    _, _, st = scene.render_count(W, H, spp=spp, seed=seed, rows=(rank, H), row_step=world)
+    _, _, st = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=step, row_band=band)
     counts = torch.tensor([traced_rays(st), algorithmic_bytes(st), st["camera"]], dtype=torch.float64, device="cuda")
     if dist:
         dist.all_reduce(counts)
@@ -152,7 +154,6 @@ def main():
     rgb = torch.empty((maxrows, W, 3), dtype=torch.float32, device="cuda")
     argb = torch.empty((maxrows, W), dtype=torch.int32, device="cuda")
     gathered = torch.empty((world, maxrows, W, 3), dtype=torch.float32, device="cuda") if dist else None
-    from distraytracer_old_amd import multigpu
     stream = torch.cuda.current_stream()
     full_img = torch.empty((H, W, 3), dtype=torch.float32, device="cuda") if dist and rank == 0 else None
 
@@ -212,7 +213,7 @@ def main():
                     f"scene scenes/{cli} (SURVEY 8(d) {args.config}); synthetic inputs where the reference's are missing",
             "config": {"workload": workload, "width": W, "height": H, "spp": spp, "seed": seed,
                        "rays_per_frame": int(rays_frame), "camera_samples": int(cam_frame),
-                       "parallelism": f"rows interleaved over {world} rank(s)" +
+                       "parallelism": f"{multigpu.BAND}-row bands interleaved over {world} rank(s)" +
                                       (" + RCCL all_gather of float RGB tiles" if world > 1 else "")},
             "camera_msamples_per_s": cam_frame / (ms_per_step / 1e3) / 1e6,
             "achieved_hbm_gbps": achieved,

@@ -59,4 +59,6 @@ struct rt_scene {
   size_t devBytes = 0;
   bool photonsUploaded = false;
   void* counters = nullptr;  // device uint64[RT_ST_N]
+  // tile schedules (longest tiles first) per tile layout: key -> device int32[tiles]
+  std::vector<std::pair<std::string, int32_t*>> schedules;
 };

@@ -146,7 +146,8 @@ struct ParamsD {
   double viewZ;
   // wave layout: G lanes per pixel (power of two, G <= spp) trace samples j, j+G, ...;
   // 64/G pixels per wave as a tw x th tile
-  int32_t G, tw, th, pad;
+  int32_t G, tw, th, band;  // band: output row ri is image row row0 + (ri/band)*rowStep*band + ri%band
+  const int32_t* order;     // tile dispatch order (longest first), nullptr = row-major
 };
 
 }  // namespace rt

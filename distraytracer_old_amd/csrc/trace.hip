@@ -189,9 +189,15 @@ static int make_params(rt_scene* s, const rt_render_params* p, ParamsD& P) {
   P.H = p->height;
   P.spp = p->spp > 0 ? p->spp : s->hs.rpp;
   if (P.spp <= 0) return set_error(RT_E_INVALID, "rays_per_pixel is 0 (scene has no fov/rays_per_pixel; Q26)");
+  const int band = p->row_band <= 1 ? 1 : p->row_band;
   P.row0 = p->row0;
   P.rowStep = step;
-  P.nrows = (row1 - p->row0 + step - 1) / step;
+  P.band = band;
+  {  // rows row0 + k*step*band + j (0 <= j < band) below row1
+    const int span = row1 - p->row0, period = step * band;
+    const int full = span / period, rest = span % period;
+    P.nrows = full * band + std::min(rest, band);
+  }
   P.seed = p->seed;
   // wave layout (render_kernel): G = largest power of two <= min(spp, 64) sample lanes per pixel
   int G = 1;
@@ -205,7 +211,7 @@ static int make_params(rt_scene* s, const rt_render_params* p, ParamsD& P) {
   P.G = G;
   P.tw = TW[lg];
   P.th = (64 / G) / P.tw;
-  P.pad = 0;
+  P.order = nullptr;
   // myFOVScene.setSceneParams (myScene.java:1367-1381) at the requested resolution
   double fov = s->hs.fov, fovRad = M_PI * fov / 180.0;
   if (std::fabs(fov - 180) < .001) fovRad -= .0001;
@@ -257,8 +263,50 @@ static RenderFn pick_variant(const HostScene& h, uint32_t flags) {
   return dv::render_kernel<false, dv::FT_ALL>;
 }
 
-static int launch(rt_scene* s, const ParamsD& P, uint32_t flags, float* d_rgb, int32_t* d_argb, bool count,
+// Dispatch schedule: tiles sorted by a probe ray's work, longest first, so the long
+// tiles do not end up in the tail of the launch (matters most for the small per-GPU
+// launches of a multi-GPU frame). Cached per tile layout; the probe and the sort run
+// once per layout (synchronously, on the first render with it).
+static int schedule(rt_scene* s, ParamsD& P, hipStream_t st) {
+  P.order = nullptr;
+  if (P.nrows * (int64_t)P.W < (1 << 16)) return RT_OK;  // small renders: row-major
+  char key[160];
+  std::snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%.17g", P.W, P.H, P.row0, P.nrows, P.rowStep, P.band,
+                P.tw, P.th, P.G, P.viewZ);
+  for (auto& e : s->schedules)
+    if (e.first == key) { P.order = e.second; return RT_OK; }
+  const int tilesX = (P.W + P.tw - 1) / P.tw, ntiles = tilesX * ((P.nrows + P.th - 1) / P.th);
+  uint32_t* d_cost = nullptr;
+  HIPCHK(hipMalloc(&d_cost, sizeof(uint32_t) * ntiles));
+  hipLaunchKernelGGL((dv::probe_kernel<dv::FT_ALL>), dim3((ntiles + 63) / 64), dim3(64), dv::LDS_BYTES, st, s->dev, P,
+                     d_cost, ntiles);
+  std::vector<uint32_t> cost(ntiles);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess) e = hipMemcpy(cost.data(), d_cost, sizeof(uint32_t) * ntiles, hipMemcpyDeviceToHost);
+  (void)hipFree(d_cost);
+  if (e != hipSuccess) return set_error(RT_E_HIP, std::string("tile probe: ") + hipGetErrorString(e));
+  std::vector<int32_t> order(ntiles);
+  for (int i = 0; i < ntiles; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+  int32_t* d_order = nullptr;
+  HIPCHK(hipMalloc(&d_order, sizeof(int32_t) * ntiles));
+  HIPCHK(hipMemcpy(d_order, order.data(), sizeof(int32_t) * ntiles, hipMemcpyHostToDevice));
+  s->allocs.push_back(d_order);
+  s->schedules.emplace_back(key, d_order);
+  P.order = d_order;
+  return RT_OK;
+}
+
+static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, int32_t* d_argb, bool count,
                   hipStream_t st) {
+  ParamsD P = P0;
+#ifndef RT_NO_SCHEDULE
+  if (!(flags & RT_RENDER_ROWMAJOR)) {
+    int rc = schedule(s, P, st);
+    if (rc) return rc;
+  }
+#endif
   int tilesX = (P.W + P.tw - 1) / P.tw, tilesY = (P.nrows + P.th - 1) / P.th;
   dim3 grid(dv::xcd_grid(tilesX * tilesY)), block(64);
   if (count) {  // counting always runs the all-features kernel

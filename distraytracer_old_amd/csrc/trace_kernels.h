@@ -1163,8 +1163,9 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   const int G = P.G;
   const int j = lane & (G - 1), pl = lane / G;
   const int tilesX = (P.W + P.tw - 1) / P.tw;
-  const int tile = tile_of_block(blockIdx.x, tilesX * ((P.nrows + P.th - 1) / P.th));
+  int tile = tile_of_block(blockIdx.x, tilesX * ((P.nrows + P.th - 1) / P.th));
   if (tile < 0) return;  // padding block of the XCD mapping (whole workgroup)
+  if (P.order) tile = P.order[tile];
   const int tx = tile % tilesX, ty = tile / tilesX;
   const int col = tx * P.tw + pl % P.tw;
   const int ri = ty * P.th + pl / P.tw;  // row index within this render's rows
@@ -1172,7 +1173,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   Counters ct;
   if (CNT)
     for (int i = 0; i < C_N; ++i) ct.c[i] = 0;
-  const int row = P.row0 + ri * P.rowStep;
+  const int row = P.row0 + (ri / P.band) * P.rowStep * P.band + ri % P.band;
   const double rayY = (-1 * (row - P.H / 2.0));
   const double rayX = col - P.W / 2.0;
   Key k;
@@ -1258,6 +1259,28 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
     for (int i = 0; i < C_N; ++i)
       if (ct.c[i]) atomicAdd(&gcount[i], (unsigned long long)ct.c[i]);
   }
+}
+
+// Tile cost probe for the dispatch schedule: one lane per tile traces the tile's first
+// pixel's un-jittered camera ray (closest hit only) and reports the work it counted.
+// Only the ORDER in which tiles are dispatched depends on it, never a pixel.
+template <uint32_t F>
+__global__ void __launch_bounds__(64) probe_kernel(SceneD S, ParamsD P, uint32_t* __restrict__ cost, int ntiles) {
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= ntiles) return;
+  const int tilesX = (P.W + P.tw - 1) / P.tw;
+  const int col = (t % tilesX) * P.tw, ri = (t / tilesX) * P.th;
+  const int row = P.row0 + (ri / P.band) * P.rowStep * P.band + ri % P.band;
+  Counters ct;
+  for (int i = 0; i < C_N; ++i) ct.c[i] = 0;
+  WRay w;
+  w.o = mk(0, 0, 0);
+  w.d = nrmz(mk(col - P.W / 2.0, -1 * (row - P.H / 2.0), P.viewZ));
+  w.d0 = w.d; w.stable = false; w.moved = false; w.ver = 0;
+  Key k;
+  k.seed = P.seed; k.pixel = (uint64_t)row * P.W + col; k.sample = 0; k.node = 1; k.tsite = SITE_TIME;
+  closest<true, F>(S, w, k, ct);
+  cost[t] = (uint32_t)(1 + ct.c[C_NODE] + ct.c[C_TRI] + ct.c[C_QUAD] + ct.c[C_IMPLICIT] + ct.c[C_TOP]);
 }
 
 // ---------------------------------------------------------------------------

@@ -1,34 +1,46 @@
 """Image partition across GPUs and the single exchange step.
 
-Rank r of N renders rows r, r+N, r+2N, ... (interleaved rows balance the
-expensive bunny/glass regions); every rank's tile is padded to ceil(H/N) rows
-so one `all_gather_into_tensor` (RCCL over xGMI; gloo in CPU tests) brings all
-float-RGB tiles to every rank, and `assemble` re-interleaves them.
+Rank r of N renders row bands r, r+N, r+2N, ... of BAND rows each (interleaved
+bands balance the expensive bunny/glass regions; bands keep a wave's 2-row pixel
+tiles on adjacent image rows, which single-row interleaving at large N would not).
+Every rank's tile is padded to the same row count (a multiple of the band) so one
+`all_gather_into_tensor` (RCCL over xGMI; gloo in CPU tests) brings all float-RGB
+tiles to every rank, and `assemble` re-interleaves them.
 
 Pixels, their RNG keys and their per-pixel sample order do not depend on N,
 so the assembled image is bit-identical to the 1-GPU image.
 """
 from __future__ import annotations
 
-
-def rows_of(rank: int, world: int, H: int) -> tuple[int, int, int]:
-    """(row0, row1, row_step) of a rank's tile."""
-    return rank, H, world
+BAND = 8  # rows per band (a multiple of every wave-tile height)
 
 
-def tile_rows(rank: int, world: int, H: int) -> int:
-    return len(range(rank, H, world))
+def rows_of(rank: int, world: int, H: int, band: int = BAND) -> tuple[int, int, int, int]:
+    """(row0, row1, row_step, row_band) of a rank's tile (rt_render_params)."""
+    return rank * band, H, world, band
 
 
-def max_tile_rows(world: int, H: int) -> int:
-    return (H + world - 1) // world
+def image_rows(rank: int, world: int, H: int, band: int = BAND) -> list[int]:
+    """Image rows of a rank's tile, in tile order."""
+    return [r for r in range(H) if (r // band) % world == rank]
 
 
-def assemble(gathered, H: int):
+def tile_rows(rank: int, world: int, H: int, band: int = BAND) -> int:
+    return len(image_rows(rank, world, H, band))
+
+
+def max_tile_rows(world: int, H: int, band: int = BAND) -> int:
+    """Padded per-rank tile height: whole bands, the same for every rank."""
+    return -(-H // (world * band)) * band
+
+
+def assemble(gathered, H: int, band: int = BAND):
     """gathered: [world, maxrows, W, C] (torch tensor or numpy array) -> [H, W, C]."""
     world, maxrows = gathered.shape[0], gathered.shape[1]
     rest = tuple(gathered.shape[2:])
-    full = gathered.swapaxes(0, 1).reshape((maxrows * world,) + rest)  # numpy and torch alike
+    k = maxrows // band
+    g = gathered.reshape((world, k, band) + rest)
+    full = g.swapaxes(0, 1).reshape((k * world * band,) + rest)  # numpy and torch alike
     return full[:H]
 
 

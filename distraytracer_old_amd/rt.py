@@ -33,7 +33,7 @@ class TextureDesc(ctypes.Structure):
 class RenderParams(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
                 ("row0", ctypes.c_int32), ("row1", ctypes.c_int32), ("row_step", ctypes.c_int32),
-                ("seed", ctypes.c_uint64), ("flags", ctypes.c_uint32), ("pad", ctypes.c_int32)]
+                ("seed", ctypes.c_uint64), ("flags", ctypes.c_uint32), ("row_band", ctypes.c_int32)]
 
 
 EXPORTS = ["rt_abi_version", "rt_last_error", "rt_device_count", "rt_scene_create", "rt_scene_load_cli",
@@ -115,17 +115,20 @@ def inspect_cli(cli: str, scene_dir=SCENE_DIR, textures: dict | None = None) -> 
 
 
 RENDER_GENERIC = 1  # RT_RENDER_GENERIC: the all-features kernel instead of the scene-specialised one
+RENDER_ROWMAJOR = 2  # RT_RENDER_ROWMAJOR: row-major tile dispatch instead of the longest-first schedule
 
 
-def params(W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, flags=0) -> RenderParams:
+def params(W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, flags=0, row_band=1) -> RenderParams:
     r0, r1 = (0, H) if rows is None else rows
-    return RenderParams(W, H, spp, r0, r1, row_step, seed, flags, 0)
+    return RenderParams(W, H, spp, r0, r1, row_step, seed, flags, row_band)
 
 
 def nrows_of(p: RenderParams) -> int:
+    """Rows row0 + k*row_step*row_band + j (0 <= j < row_band) below row1."""
     r1 = p.row1 if p.row1 > 0 else p.height
-    step = max(1, p.row_step)
-    return (r1 - p.row0 + step - 1) // step
+    step, band = max(1, p.row_step), max(1, p.row_band)
+    full, rest = divmod(r1 - p.row0, step * band)
+    return full * band + min(rest, band)
 
 
 class Scene:
@@ -174,16 +177,16 @@ class Scene:
         _check(lib().rt_scene_photons(self._h, pos.ctypes.data, pwr.ctypes.data, n, ctypes.byref(cnt)), "rt_scene_photons")
         return pos, pwr
 
-    def render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, flags=0):
-        p = params(W, H, spp, seed, rows, row_step, flags)
+    def render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, flags=0, row_band=1):
+        p = params(W, H, spp, seed, rows, row_step, flags, row_band)
         n = nrows_of(p)
         rgb = np.zeros((n, W, 3), dtype=np.float32)
         argb = np.zeros((n, W), dtype=np.int32)
         _check(lib().rt_render(self._h, ctypes.byref(p), rgb.ctypes.data, argb.ctypes.data), "rt_render")
         return rgb, argb
 
-    def render_count(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1):
-        p = params(W, H, spp, seed, rows, row_step)
+    def render_count(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, row_band=1):
+        p = params(W, H, spp, seed, rows, row_step, 0, row_band)
         n = nrows_of(p)
         rgb = np.zeros((n, W, 3), dtype=np.float32)
         argb = np.zeros((n, W), dtype=np.int32)
@@ -197,8 +200,9 @@ class Scene:
         _check(lib().rt_render_device(self._h, ctypes.byref(p), ctypes.c_void_p(rgb_ptr), ctypes.c_void_p(argb_ptr),
                                       ctypes.c_void_p(stream)), "rt_render_device")
 
-    def time_render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, warmup=1, iters=3, flags=0) -> float:
-        p = params(W, H, spp, seed, rows, row_step, flags)
+    def time_render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, warmup=1, iters=3, flags=0,
+                    row_band=1) -> float:
+        p = params(W, H, spp, seed, rows, row_step, flags, row_band)
         ms = ctypes.c_double(0)
         _check(lib().rt_time_render(self._h, ctypes.byref(p), warmup, iters, ctypes.byref(ms)), "rt_time_render")
         return ms.value

@@ -136,15 +136,19 @@ typedef struct rt_render_params {
   int32_t width, height; /* image size (the reference hard-codes 300x300, DistRayTracer.java:15-16) */
   int32_t spp;           /* <= 0: the scene's rays_per_pixel */
   int32_t row0, row1;    /* rows [row0,row1) of the image; row1 <= 0 means height */
-  int32_t row_step;      /* <= 1: every row; >1: interleaved rows (multi-GPU bands) */
+  int32_t row_step;      /* <= 1: every row; >1: interleaved bands (multi-GPU) */
   uint64_t seed;         /* keyed RNG seed */
   uint32_t flags;        /* RT_RENDER_* */
-  int32_t pad;
+  int32_t row_band;      /* <= 1: single rows. The rendered rows are row0 + k*row_step*row_band + j,
+                            0 <= j < row_band, below row1; output row i is the i-th of them */
 } rt_render_params;
 
 /* rt_render_params.flags: run the all-features kernel instead of the one specialised
    to the scene's features (results are identical; for testing the specialisation) */
 #define RT_RENDER_GENERIC 1u
+/* dispatch tiles in row-major order instead of the probed longest-first schedule
+   (results are identical; for testing and timing the schedule) */
+#define RT_RENDER_ROWMAJOR 2u
 
 typedef struct rt_scene rt_scene;
 

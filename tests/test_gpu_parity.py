@@ -158,3 +158,24 @@ def test_photon_shards_merge_to_the_full_prepass(tmp_path):
     a = full.render(64, 64, spp=2, seed=seed)
     b = sh.render(64, 64, spp=2, seed=seed)
     assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0])
+
+
+def test_rank_bands_equal_full_image_rows():
+    """A rank's banded tile (multi-GPU partition, 8(e)) is exactly its rows of the 1-GPU image."""
+    from distraytracer_old_amd import multigpu
+    tex = scenes.prepare("c3_bun69k.cli")
+    g = rt.Scene.load_cli("c3_bun69k.cli", textures=tex)
+    full, af = g.render(256, 256, spp=4, seed=SEED)
+    for world, rank in [(8, 3), (3, 2)]:
+        r0, r1, step, band = multigpu.rows_of(rank, world, 256)
+        tile, at = g.render(256, 256, spp=4, seed=SEED, rows=(r0, r1), row_step=step, row_band=band)
+        rows = multigpu.image_rows(rank, world, 256)
+        assert np.array_equal(tile, full[rows]) and np.array_equal(at, af[rows])
+
+
+def test_tile_schedule_does_not_change_the_image():
+    """The probed longest-first tile dispatch order renders bit-identically to row-major."""
+    g = rt.Scene.load_cli("c3_bun69k.cli", textures=scenes.prepare("c3_bun69k.cli"))
+    a, aa = g.render(512, 512, spp=2, seed=SEED)
+    b, ab = g.render(512, 512, spp=2, seed=SEED, flags=rt.RENDER_ROWMAJOR)
+    assert np.array_equal(aa, ab) and np.array_equal(a.view(np.uint32), b.view(np.uint32))

@@ -32,12 +32,17 @@ def _worker(rank, world, port, H, W, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     o = OracleScene(scenes.SCENE_DIR, "c3shinyBall.cli", scenes.prepare("c3shinyBall.cli"))
-    r0, r1, step = multigpu.rows_of(rank, world, H)
-    rgb, _, _ = o.render(W, H, spp=2, seed=11, rows=(r0, r1), row_step=step, threads=2)
-    tile = torch.zeros((multigpu.max_tile_rows(world, H), W, 3), dtype=torch.float32)
+    band = 3
+    rows = multigpu.image_rows(rank, world, H, band)
+    # the oracle renders the rank's bands one by one (the HIP kernel does them in one launch)
+    parts = [o.render(W, H, spp=2, seed=11, rows=(b0, min(b0 + band, H)), threads=2)[0]
+             for b0 in rows[::band]]
+    rgb = np.concatenate(parts)
+    assert rgb.shape[0] == len(rows)
+    tile = torch.zeros((multigpu.max_tile_rows(world, H, band), W, 3), dtype=torch.float32)
     tile[: rgb.shape[0]] = torch.from_numpy(rgb)
     g = multigpu.gather_tiles(tile, dist)
-    full = multigpu.assemble(g, H)
+    full = multigpu.assemble(g, H, band)
     if rank == 0:
         q.put(full.numpy())
     dist.barrier()
@@ -64,14 +69,25 @@ def test_gloo_world2_gather_equals_single_image():
 
 
 def test_assemble_numpy_ragged():
-    H, W, world = 10, 3, 4
-    img = np.arange(H * W).reshape(H, W, 1)
-    tiles = np.zeros((world, multigpu.max_tile_rows(world, H), W, 1), dtype=img.dtype)
-    for r in range(world):
-        rows = img[r::world]
-        tiles[r, : rows.shape[0]] = rows
-        assert rows.shape[0] == multigpu.tile_rows(r, world, H)
-    assert np.array_equal(multigpu.assemble(tiles, H), img)
+    for H, W, world, band in [(10, 3, 4, 1), (37, 5, 3, 4), (1024, 2, 8, 8), (19, 2, 8, 8)]:
+        img = np.arange(H * W).reshape(H, W, 1)
+        tiles = np.zeros((world, multigpu.max_tile_rows(world, H, band), W, 1), dtype=img.dtype)
+        for r in range(world):
+            rows = img[multigpu.image_rows(r, world, H, band)]
+            tiles[r, : rows.shape[0]] = rows
+            assert rows.shape[0] == multigpu.tile_rows(r, world, H, band)
+        assert np.array_equal(multigpu.assemble(tiles, H, band), img)
+
+
+def test_row_band_params_match_partition():
+    """rt_render_params (row0, row_step, row_band) select exactly multigpu.image_rows."""
+    from distraytracer_old_amd import rt
+    for H, world, band in [(1024, 8, 8), (37, 3, 4), (300, 2, 8), (10, 4, 1)]:
+        for rank in range(world):
+            r0, r1, step, b = multigpu.rows_of(rank, world, H, band)
+            p = rt.params(64, H, rows=(r0, r1), row_step=step, row_band=b)
+            rows = [r0 + (i // b) * step * b + i % b for i in range(rt.nrows_of(p))]
+            assert rows == multigpu.image_rows(rank, world, H, band)
 
 
 def test_merge_photon_shards_restores_insertion_order():

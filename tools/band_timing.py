@@ -1,0 +1,23 @@
+#!/usr/bin/env python3
+"""Per-rank kernel time of the multi-GPU row-band partition, emulated on one GPU: max over
+ranks vs full-frame/N (strong-scaling efficiency of the kernel alone), with the probed
+longest-first tile schedule and with row-major dispatch."""
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from distraytracer_old_amd import multigpu, rt, scenes  # noqa: E402
+
+scenes.ensure_bun69k()
+s = rt.Scene.load_cli("c3_bun69k.cli", textures=scenes.prepare("c3_bun69k.cli"))
+for flags, name in ((0, "schedule"), (rt.RENDER_ROWMAJOR, "row-major")):
+    full = s.time_render(1024, 1024, spp=16, seed=0x5EED0001, iters=5, flags=flags)
+    print(name, "full %.3f ms" % full)
+    for world in (2, 4, 8):
+        ts = []
+        for rank in range(world):
+            r0, r1, step, b = multigpu.rows_of(rank, world, 1024)
+            ts.append(s.time_render(1024, 1024, spp=16, seed=0x5EED0001, rows=(r0, r1), row_step=step, row_band=b,
+                                    iters=5, flags=flags))
+        print(" ", world, "max %.3f mean %.3f ideal %.3f eff %.3f" % (max(ts), sum(ts) / len(ts), full / world,
+                                                                       full / world / max(ts)))
