@@ -6,7 +6,7 @@
 // would hand over, then calls rt_scene_create().
 //
 // Commands outside the hot-path scope (instances, sierpinski, wood/stone
-// textures, fisheye/ortho cameras) are rejected with RT_E_PARSE.
+// textures) are rejected with RT_E_PARSE.
 #include <cctype>
 #include <fstream>
 #include <map>
@@ -162,6 +162,19 @@ struct CliLoader {
           if (!isMain) continue;
           d.rays_per_pixel = (curRpp != 0) ? curRpp : 1;
           d.fov = num(t, 1);
+          d.camera = RT_CAMERA_FOV;
+        } else if (c == "fisheye" || c == "fishEye") {  // :66-74 (myFishEyeScene)
+          if (!isMain) continue;
+          d.rays_per_pixel = (curRpp != 0) ? curRpp : 1;
+          d.camera = RT_CAMERA_FISHEYE;
+          d.camera_param[0] = num(t, 1);
+          d.camera_param[1] = 0;
+        } else if (c == "ortho" || c == "orthographic") {  // :75-83 (myOrthoScene)
+          if (!isMain) continue;
+          d.rays_per_pixel = (curRpp != 0) ? curRpp : 1;
+          d.camera = RT_CAMERA_ORTHO;
+          d.camera_param[0] = num(t, 1);
+          d.camera_param[1] = num(t, 2);
         } else if (c == "lens") {
           d.dof = 1; d.lens_radius = num(t, 1); d.lens_focal = num(t, 2);
         } else if (c == "write") {

@@ -38,6 +38,8 @@ struct HostScene {
   double sky[4] = {0, 0, 0, 0};
   int dof = 0;
   double lensRadius = 0, lensFocal = 0;
+  int camera = 0;  // RT_CAMERA_*
+  double cameraParam[2] = {0, 0};
   int rpp = 0;
   int photonMode = 0, photonCount = 0, photonK = 0;
   double photonMaxD2 = 0;

@@ -429,6 +429,10 @@ struct Builder {
     hs.bkgTex = d->bkg_texture;
     for (int c = 0; c < 4; ++c) hs.sky[c] = d->skydome[c];
     hs.dof = d->dof; hs.lensRadius = d->lens_radius; hs.lensFocal = d->lens_focal;
+    if (d->camera < RT_CAMERA_FOV || d->camera > RT_CAMERA_ORTHO) { err = "bad camera type"; return false; }
+    hs.camera = d->camera;
+    hs.cameraParam[0] = d->camera_param[0]; hs.cameraParam[1] = d->camera_param[1];
+    if (hs.camera != RT_CAMERA_FOV) hs.dof = 0;  // only myFOVScene.draw uses the lens
     hs.rpp = d->rays_per_pixel;
     hs.photonMode = d->photon_mode; hs.photonCount = d->photon_count; hs.photonK = d->photon_k;
     hs.photonMaxD2 = d->photon_max_dist * d->photon_max_dist;

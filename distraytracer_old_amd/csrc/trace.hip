@@ -216,6 +216,19 @@ static int make_params(rt_scene* s, const rt_render_params* p, ParamsD& P) {
   double fov = s->hs.fov, fovRad = M_PI * fov / 180.0;
   if (std::fabs(fov - 180) < .001) fovRad -= .0001;
   P.viewZ = -1 * (std::max(P.H, P.W) / 2.0) / std::tan(fovRad / 2);
+  // myFishEyeScene / myOrthoScene constants (setImageSize :780-792, setSceneParams :1556-1560, :1683-1688)
+  P.cam = s->hs.camera;
+  P.pad2 = 0;
+  {
+    const double maxDim = std::max(P.H, P.W), rayYOffset = P.H / 2.0, rayXOffset = P.W / 2.0;
+    P.yStart = ((maxDim - P.H) / 2.0) - rayYOffset;
+    P.xStart = ((maxDim - P.W) / 2.0) - rayXOffset;
+    P.fishMult = 2.0 / maxDim;
+    P.aperHalf = (M_PI * s->hs.cameraParam[0] / 180.0) / 2.0;
+    const double div = std::min(P.W, P.H);  // the reference divides by the applet's (= image) size
+    P.orthPerRow = s->hs.cameraParam[1] / div;
+    P.orthPerCol = s->hs.cameraParam[0] / div;
+  }
   if (s->hs.photonMode && !s->photonsUploaded) {
     int rc = rt_photons_build(s, p->seed);
     if (rc) return rc;
@@ -230,6 +243,7 @@ static uint32_t scene_features(const HostScene& h) {
   if (h.bkgTex >= 0) f |= dv::FT_TEX;
   if (h.photonMode) f |= dv::FT_PHOTON;
   if (h.dof) f |= dv::FT_DOF;
+  if (h.camera != RT_CAMERA_FOV) f |= dv::FT_CAMX;
   for (const MatD& m : h.mat) {
     if (m.tex != 0) f |= dv::FT_TEX;
     if (m.usePhotonMap) f |= dv::FT_PHOTON;

@@ -25,7 +25,8 @@ enum : uint32_t {
   FT_TRANS = 8,   // transparent materials (Fresnel split, two children per node)
   FT_DOF = 16,    // lens / depth of field
   FT_LIGHTX = 32, // spot or disk lights
-  FT_ALL = 63
+  FT_CAMX = 64,   // fisheye or orthographic camera
+  FT_ALL = 127
 };
 
 __constant__ int c_perm[256];
@@ -112,7 +113,7 @@ static constexpr int STK_LDS = RT_STACK_LDS;
 // per-round sample colours (used only between traversals)
 extern __shared__ double rt_lds[];
 static constexpr int LDS_STACK_BYTES = STK_LDS * 64 * 12;
-static constexpr int LDS_BYTES = LDS_STACK_BYTES > 64 * 3 * 8 ? LDS_STACK_BYTES : 64 * 3 * 8;
+static constexpr int LDS_BYTES = LDS_STACK_BYTES > 64 * 4 * 8 ? LDS_STACK_BYTES : 64 * 4 * 8;
 typedef __attribute__((address_space(3))) double lds_f64;
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 DEVI lds_f64* ldsT() { return (lds_f64*)rt_lds; }
@@ -1158,7 +1159,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   // loads, little divergence). Lane j of a pixel traces samples j, j+G, ...; each round's
   // G colours go through LDS and the pixel's first lane adds them in sample order, so
   // the per-pixel sum is the reference's sequential sum (myScene.java:1451-1460).
-  double* cbuf = rt_lds;  // 64 x 3 doubles, aliases the traversal stack
+  double* cbuf = rt_lds;  // 64 x 4 doubles (colour, traced), aliases the traversal stack
   const int lane = threadIdx.x;
   const int G = P.G;
   const int j = lane & (G - 1), pl = lane / G;
@@ -1181,7 +1182,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   k.pixel = (uint64_t)row * (uint64_t)P.W + (uint64_t)col;
   k.tsite = SITE_TIME;
   const int n = P.spp;
-  const bool dof = (F & FT_DOF) && S.dof;
+  const bool dof = (F & FT_DOF) && S.dof && !((F & FT_CAMX) && P.cam != 0);
   V fpt = mk(0, 0, 0), lc = mk(0, 0, 0);
   if (dof && valid) {  // shootMultiDpthOfFldRays (myScene.java:1386-1406)
     lc = nrmz(mk(rayX, rayY, P.viewZ));
@@ -1200,9 +1201,41 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   for (int s0 = 0; s0 < n; s0 += G) {
     const int s = s0 + j;
     V cc = mk(0, 0, 0);
+    bool traced = false;  // a fisheye sample outside the image circle adds nothing (myScene.java:1571)
     if (valid && s < n) {
       V o, d;
-      if (dof) {
+      traced = true;
+      if ((F & FT_CAMX) && P.cam == 1) {  // myFishEyeScene: draw (1 spp) :1605-1622 / shootMultiRays :1562-1583
+        double xVal, yVal, rSq;
+        if (n == 1) {
+          yVal = (row + P.yStart) * P.fishMult;
+          const double ySq = yVal * yVal;
+          xVal = (col + P.xStart) * P.fishMult;
+          rSq = xVal * xVal + ySq;
+          traced = !(rSq > 1);  // outside: blkColor
+        } else {
+          yVal = ((row + P.yStart) + rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_AA_Y, 0, -.5, .5)) * P.fishMult;
+          xVal = ((col + P.xStart) + rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_AA_X, 0, -.5, .5)) * P.fishMult;
+          rSq = yVal * yVal + xVal * xVal;
+          traced = rSq <= 1;
+        }
+        const double r = sqrt(rSq), theta = r * P.aperHalf, phi = atan2(-yVal, xVal), sTh = sin(theta);
+        o = mk(0, 0, 0);
+        d = mk(sTh * cos(phi), sTh * sin(phi), -cos(theta));
+      } else if ((F & FT_CAMX) && P.cam == 2) {  // myOrthoScene: draw :1704-1745 / shootMultiRays :1690-1702
+        const double rayYOffset = P.H / 2.0, rayXOffset = P.W / 2.0;
+        double rx, ry;
+        if (n == 1) {
+          ry = P.orthPerRow * (-1 * (row - rayYOffset));
+          rx = P.orthPerCol * (col - rayXOffset);
+        } else {
+          const double yB = P.orthPerRow * ((-1 * (row - rayYOffset)) - .5), xB = P.orthPerCol * (col - rayXOffset - .5);
+          ry = yB + (P.orthPerRow * rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_AA_Y, 0, -.5, .5));
+          rx = xB + (P.orthPerCol * rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_AA_X, 0, -.5, .5));
+        }
+        o = mk(rx, ry, 0);
+        d = mk(0, 0, -1);
+      } else if (dof) {
         double th = rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_DOF_ANG, 0, 0, TWO_PI_F);
         V tt = nrmz(rot_axis(mk(0, 1, 0), mk(0, 0, -1), th));
         double mm = rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_DOF_RAD, 0, 0, S.lensRadius);
@@ -1218,24 +1251,27 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
         o = mk(0, 0, 0);
         d = mk(rx, ry, P.viewZ);
       }
-      Key ks = k;
-      ks.sample = (uint32_t)s;
-      if (CNT) ct.c[C_CAMERA]++;
-      cc = trace_sample<CNT, F>(S, o, d, ks, ct);
+      if (traced) {
+        Key ks = k;
+        ks.sample = (uint32_t)s;
+        if (CNT) ct.c[C_CAMERA]++;
+        cc = trace_sample<CNT, F>(S, o, d, ks, ct);
+      }
     }
     if (G == 1) {
       c1 = cc;
-      rs += cc.x; gs += cc.y; bs += cc.z;
+      if (traced) { rs += cc.x; gs += cc.y; bs += cc.z; }
     } else {
-      cbuf[3 * lane + 0] = cc.x;
-      cbuf[3 * lane + 1] = cc.y;
-      cbuf[3 * lane + 2] = cc.z;
+      cbuf[4 * lane + 0] = cc.x;
+      cbuf[4 * lane + 1] = cc.y;
+      cbuf[4 * lane + 2] = cc.z;
+      cbuf[4 * lane + 3] = traced ? 1.0 : 0.0;
       __syncthreads();
       if (j == 0) {
         const int m = (n - s0) < G ? (n - s0) : G;
         for (int q = 0; q < m; ++q) {
-          const double* b = cbuf + 3 * (pl * G + q);
-          rs += b[0]; gs += b[1]; bs += b[2];
+          const double* b = cbuf + 4 * (pl * G + q);
+          if (b[3] != 0) { rs += b[0]; gs += b[1]; bs += b[2]; }
         }
       }
       __syncthreads();

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum rt_status {
   RT_OK = 0,
@@ -125,12 +125,17 @@ typedef struct rt_scene_desc {
   int32_t bkg_texture;   /* -1 none; else skydome texture index */
   int32_t rays_per_pixel;
   double skydome[4];     /* radius, cx, cy, cz */
-  int32_t dof, pad0;
+  int32_t dof;           /* lens set: depth of field (FOV camera only, myFOVScene.draw) */
+  int32_t camera;        /* RT_CAMERA_*: the scene subclass the .cli selected (myRTFileReader.java:51-83) */
   double lens_radius, lens_focal;
   int32_t photon_mode;   /* 0 none, 1 diffuse_photons, 2 caustic_photons */
   int32_t photon_count, photon_k, pad1;
   double photon_max_dist; /* already rounded through float (Float.parseFloat) */
+  double camera_param[2];  /* RT_CAMERA_FISHEYE: {aperture degrees, 0}; RT_CAMERA_ORTHO: {width, height} */
 } rt_scene_desc;
+
+/* rt_scene_desc.camera */
+enum { RT_CAMERA_FOV = 0, RT_CAMERA_FISHEYE = 1, RT_CAMERA_ORTHO = 2 };
 
 typedef struct rt_render_params {
   int32_t width, height; /* image size (the reference hard-codes 300x300, DistRayTracer.java:15-16) */

@@ -745,6 +745,9 @@ struct Scene {
   int numRaysPerPixel = 0;
   int numRays = 8, numPhotonRays = 4;
   double fov = 60, viewZ = -1;
+  // camera: 0 myFOVScene, 1 myFishEyeScene (fishEye degrees), 2 myOrthoScene (width, height)
+  int camType = 0;
+  double fishEye = 0, orthoW = 0, orthoH = 0;
   Color backgroundColor;
   bool txtrdBkg = false;
   Sphere* skyDome = nullptr;
@@ -1542,6 +1545,18 @@ struct Loader {
           if (!isMain) continue;
           s->numRaysPerPixel = (curNumRaysPerPxl != 0) ? curNumRaysPerPxl : 1;
           s->fov = num(t, 1);
+          s->camType = 0;
+        } else if (c == "fisheye" || c == "fishEye") {  // myRTFileReader.java:66-74
+          if (!isMain) continue;
+          s->numRaysPerPixel = (curNumRaysPerPxl != 0) ? curNumRaysPerPxl : 1;
+          s->camType = 1;
+          s->fishEye = num(t, 1);
+        } else if (c == "ortho" || c == "orthographic") {  // myRTFileReader.java:75-83
+          if (!isMain) continue;
+          s->numRaysPerPixel = (curNumRaysPerPxl != 0) ? curNumRaysPerPxl : 1;
+          s->camType = 2;
+          s->orthoW = num(t, 1);
+          s->orthoH = num(t, 2);
         } else if (c == "lens") {
           s->hasDOF = true; s->lensRadius = num(t, 1); s->lensFocal = num(t, 2);
         } else if (c == "write") {
@@ -1826,10 +1841,10 @@ struct Loader {
           R2.m[1][1] = std::cos(ar); R2.m[1][2] = -std::sin(ar); R2.m[2][1] = std::sin(ar); R2.m[2][2] = std::cos(ar);
           M4 tmp = mmul(R2, R1);
           stack.back() = mmul(stack.back(), mmul(R1T, tmp));
-        } else if (c == "reset_timer" || c == "print_timer" || c == "refine" || c == "fisheye" || c == "fishEye") {
+        } else if (c == "reset_timer" || c == "print_timer" || c == "refine") {
           // timers and the progressive `refine` preview are ignored (documented override)
         } else {
-          // other commands (instances, sierpinski, ortho, ...) are outside the hot-path scope
+          // other commands (instances, sierpinski, ...) are outside the hot-path scope
           err = "unsupported command: " + c;
           return false;
         }
@@ -1943,7 +1958,58 @@ int oracle_render(void* p, int W, int H, int spp, uint64_t seed, int row0, int r
       double rayX = col - rayXOffset;
       uint64_t pix = (uint64_t)row * (uint64_t)W + (uint64_t)col;
       Color c;
-      if (s->hasDOF) {  // shootMultiDpthOfFldRays :1386-1406
+      if (s->camType == 1) {  // myFishEyeScene.draw / shootMultiRays (myScene.java:1562-1653)
+        const double maxDim = std::max(H, W);
+        const double yStart = ((maxDim - H) / 2.0) - rayYOffset, xStart = ((maxDim - W) / 2.0) - rayXOffset;
+        const double fishMult = 2.0 / maxDim;  // setImageSize :780-792
+        const double aperatureHlf = (M_PI * s->fishEye / 180.0) / 2.0;
+        auto fish_ray = [&](double xVal, double yVal, double rSq, uint32_t k) -> Color {
+          double r = std::sqrt(rSq), theta = r * aperatureHlf, phi = std::atan2(-yVal, xVal), sTh = std::sin(theta);
+          Ray ray(V3(0, 0, 0), V3(sTh * std::cos(phi), sTh * std::sin(phi), -std::cos(theta)), 0);
+          ray.key.seed = seed; ray.key.pixel = pix; ray.key.sample = k; ray.key.node = 1;
+          st[ST_CAM]++;
+          return reflect_ray(s, ray, st);
+        };
+        if (n == 1) {
+          double yVal = (row + yStart) * fishMult, ySq = yVal * yVal, xVal = (col + xStart) * fishMult;
+          double rTmp = xVal * xVal + ySq;
+          c = (rTmp > 1) ? Color(0, 0, 0) : fish_ray(xVal, yVal, rTmp, 0);  // blkColor outside the circle
+        } else {
+          double yB = row + yStart, xB = col + xStart, rs = 0, gs = 0, bs = 0;
+          for (int k = 0; k < n; ++k) {
+            double yVal = (yB + rng_range(rng_bits(seed, pix, (uint32_t)k, 0, SITE_AA_Y, 0), -.5, .5)) * fishMult;
+            double xVal = (xB + rng_range(rng_bits(seed, pix, (uint32_t)k, 0, SITE_AA_X, 0), -.5, .5)) * fishMult;
+            double rSq = yVal * yVal + xVal * xVal;
+            if (rSq <= 1) {
+              Color cc = fish_ray(xVal, yVal, rSq, (uint32_t)k);
+              rs += cc.r; gs += cc.g; bs += cc.b;
+            }
+          }
+          c = Color(rs / n, gs / n, bs / n);
+        }
+      } else if (s->camType == 2) {  // myOrthoScene.draw / shootMultiRays (myScene.java:1690-1753)
+        const double div = std::min(W, H);  // the reference divides by the applet's (= image) size
+        const double orthPerRow = s->orthoH / div, orthPerCol = s->orthoW / div;
+        auto ortho_ray = [&](double rx, double ry, uint32_t k) -> Color {
+          Ray ray(V3(rx, ry, 0), V3(0, 0, -1), 0);
+          ray.key.seed = seed; ray.key.pixel = pix; ray.key.sample = k; ray.key.node = 1;
+          st[ST_CAM]++;
+          return reflect_ray(s, ray, st);
+        };
+        if (n == 1) {
+          c = ortho_ray(orthPerCol * (col - rayXOffset), orthPerRow * (-1 * (row - rayYOffset)), 0);
+        } else {
+          double yB = orthPerRow * ((-1 * (row - rayYOffset)) - .5), xB = orthPerCol * (col - rayXOffset - .5);
+          double rs = 0, gs = 0, bs = 0;
+          for (int k = 0; k < n; ++k) {
+            double ry = yB + (orthPerRow * rng_range(rng_bits(seed, pix, (uint32_t)k, 0, SITE_AA_Y, 0), -.5, .5));
+            double rx = xB + (orthPerCol * rng_range(rng_bits(seed, pix, (uint32_t)k, 0, SITE_AA_X, 0), -.5, .5));
+            Color cc = ortho_ray(rx, ry, (uint32_t)k);
+            rs += cc.r; gs += cc.g; bs += cc.b;
+          }
+          c = Color(rs / n, gs / n, bs / n);
+        }
+      } else if (s->hasDOF) {  // shootMultiDpthOfFldRays :1386-1406
         V3 lc(rayX, rayY, s->viewZ);
         normalize_ip(lc);
         Ray ray(V3(0, 0, 0), lc, 0);

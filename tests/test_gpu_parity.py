@@ -58,6 +58,18 @@ def test_c4_planets_small_parity():
     assert c["mismatch_frac"] < 2e-3, c
 
 
+@pytest.mark.parametrize("cli,spp", [("old_t07.cli", 1), ("old_t07.cli", 4), ("old_t10.cli", 1), ("old_t10.cli", 4),
+                                     ("planets3Ortho.cli", 2)])
+def test_camera_scenes_parity(cli, spp):
+    """orthographic (old_t07, planets3Ortho: textures + glass) and fisheye 180 (old_t10) cameras
+    (myOrthoScene / myFishEyeScene, myScene.java:1535-1755), 1 spp and jittered."""
+    g, o, (rg, ag), (ro, ao) = both(cli, 96, 96, spp)
+    c = compare(rg, ag, ro, ao)
+    assert c["mismatch_frac"] < 2e-3, c
+    if cli == "old_t10.cli" and spp == 1:  # outside the image circle: blkColor
+        assert (int(ag[0, 0]) & 0xFFFFFFFF) == 0xFF000000 and rg[0, 0].max() == 0
+
+
 @pytest.mark.parametrize("cli,spp", [("p2_t05.cli", 4), ("p2_t07.cli", 4), ("c2clear.cli", 1), ("p2_t03.cli", 4)])
 def test_feature_scenes_parity(cli, spp):
     """disk light (p2_t05), depth of field (p2_t07), refraction (c2clear), motion blur (p2_t03)."""

@@ -74,3 +74,22 @@ def test_photon_map_builds_kdtree():
         assert st["photon"] > 0 and np.isfinite(rgb).all()
     finally:
         shutil.rmtree(d)
+
+
+def test_kat_ortho_and_fisheye_centre():
+    """Hand-derived KAT (myOrthoScene / myFishEyeScene, myScene.java:1535-1755): the centre
+    pixel's ray runs down -z in both old_t07 (ortho 6 6, origin (0,0,0)) and old_t10 (fisheye
+    180: r = 0 -> theta = 0 -> d = (0,0,-1)); it hits the unit sphere at (0,0,-6) in
+    P = (0,0,-5), N = (0,0,1); light (0,0,0) .2 gives .8*.2*1, light (4,4,0) 1 gives
+    .8*(N.L = 5/sqrt(57)); ambient 0 -> 0.16 + 0.8*5/sqrt(57) = 0.689813 -> 0xFFAFAFAF.
+    A fisheye pixel outside the image circle is blkColor (0xFF000000)."""
+    expect = 0.16 + 0.8 * 5 / np.sqrt(57)
+    for cli in ("old_t07.cli", "old_t10.cli"):
+        o = OracleScene(scenes.SCENE_DIR, cli, {})
+        rgb, argb, _ = o.render(300, 300, spp=1, rows=(150, 151))
+        assert np.allclose(rgb[0, 150], expect, atol=1e-6)
+        assert (int(argb[0, 150]) & 0xFFFFFFFF) == 0xFFAFAFAF
+    o = OracleScene(scenes.SCENE_DIR, "old_t10.cli", {})
+    _, argb, st = o.render(300, 300, spp=1, rows=(0, 1))
+    assert (int(argb[0, 0]) & 0xFFFFFFFF) == 0xFF000000
+    assert st["camera"] < 300  # corners of the top row lie outside the circle and trace nothing
