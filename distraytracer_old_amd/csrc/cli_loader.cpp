@@ -5,8 +5,8 @@
 // stack). It emits the flattened rt_scene_desc that a JNI myScene subclass
 // would hand over, then calls rt_scene_create().
 //
-// Commands outside the hot-path scope (instances, sierpinski, wood/stone
-// textures) are rejected with RT_E_PARSE.
+// Commands outside the hot-path scope (instances, sierpinski, the cellular
+// `stone` texture) are rejected with RT_E_PARSE.
 #include <cctype>
 #include <fstream>
 #include <map>
@@ -28,6 +28,34 @@ struct Clr {
 };
 static Clr clr(double r, double g, double b) { return Clr{jmin(1, r), jmin(1, g), jmin(1, b)}; }  // myColor clamp
 
+// DistRayTracer.getClr (DistRayTracer.java:467-530): named colours of `noise_color`
+// (clr_rnd draws from Processing's unseeded random: rejected)
+static bool named_color(std::string n, Clr& c) {
+  for (auto& ch : n) ch = (char)std::tolower(ch);
+  static const std::map<std::string, Clr> tab = {
+      {"clr_gray", {0.47, 0.47, 0.47}}, {"clr_white", {1.0, 1.0, 1.0}}, {"clr_yellow", {1.0, 1.0, 0}},
+      {"clr_cyan", {0, 1.0, 1.0}}, {"clr_magenta", {1.0, 0, 1.0}}, {"clr_red", {1.0, 0, 0}}, {"clr_blue", {0, 0, 1.0}},
+      {"clr_purple", {0.6, 0.2, 1.0}}, {"clr_green", {0, 1.0, 0}}, {"clr_ltwood1", {0.94, 0.47, 0.12}},
+      {"clr_ltwood2", {0.94, 0.8, 0.4}}, {"clr_dkwood1", {0.2, 0.08, 0.08}}, {"clr_dkwood2", {0.3, 0.20, 0.16}},
+      {"clr_mortar1", {0.2, 0.2, 0.2}}, {"clr_mortar2", {0.7, 0.7, 0.7}}, {"clr_brick1_1", {0.6, 0.18, 0.22}},
+      {"clr_brick1_2", {0.8, 0.26, 0.33}}, {"clr_brick2_1", {0.6, 0.32, 0.16}}, {"clr_brick2_2", {0.8, 0.45, 0.25}},
+      {"clr_brick3_1", {0.3, 0.01, 0.07}}, {"clr_brick3_2", {0.6, 0.02, 0.13}}, {"clr_brick4_1", {0.4, 0.1, 0.17}},
+      {"clr_brick4_2", {0.6, 0.3, 0.13}}, {"clr_darkgray", {0.31, 0.31, 0.31}}, {"clr_darkred", {0.47, 0, 0}},
+      {"clr_darkblue", {0, 0, 0.47}}, {"clr_darkpurple", {0.4, 0.2, 0.6}}, {"clr_darkgreen", {0, 0.47, 0}},
+      {"clr_darkyellow", {0.47, 0.47, 0}}, {"clr_darkmagenta", {0.47, 0, 0.47}}, {"clr_darkcyan", {0, 0.47, 0.47}},
+      {"clr_lightgray", {0.78, 0.78, 0.78}}, {"clr_lightred", {1.0, .43, .43}}, {"clr_lightblue", {0.43, 0.43, 1.0}},
+      {"clr_lightgreen", {0.43, 1.0, 0.43}}, {"clr_lightyellow", {1.0, 1.0, .43}}, {"clr_lightmagenta", {1.0, .43, 1.0}},
+      {"clr_lightcyan", {0.43, 1.0, 1.0}}, {"clr_black", {0, 0, 0}}, {"clr_nearblack", {0.05, 0.05, 0.05}},
+      {"clr_faintgray", {0.43, 0.43, 0.43}}, {"clr_faintred", {0.43, 0, 0}}, {"clr_faintblue", {0, 0, 0.43}},
+      {"clr_faintgreen", {0, 0.43, 0}}, {"clr_faintyellow", {0.43, 0.43, 0}}, {"clr_faintcyan", {0, 0.43, 0.43}},
+      {"clr_faintmagenta", {0.43, 0, 0.43}}, {"clr_offwhite", {0.95, 0.98, 0.92}}};
+  auto it = tab.find(n);
+  if (it != tab.end()) { c = it->second; return true; }
+  if (n == "clr_rnd") return false;
+  c = clr(1.0, 1.0, 1.0);  // "Color not found ... so using white"
+  return true;
+}
+
 struct CliLoader {
   std::string dir;
   std::map<std::string, int> texIndex;
@@ -43,6 +71,7 @@ struct CliLoader {
   D3 pdMult{10, 10, 10};
   bool rndColors = false, useFwdTrans = false, useCustClrs = false;
   Clr colors[2] = {clr(.7, .7, .7), clr(.2, .2, .2)};
+  int ncust = 0;  // noise_color entries since the last reset
   bool photonMap = false, caustic = false;
   // accumulated desc
   std::vector<rt_prim_desc> prims;
@@ -67,7 +96,7 @@ struct CliLoader {
     rt_material_desc m;
     std::memset(&m, 0, sizeof(m));
     m.simple = simple;
-    m.texture = (txtrType == 1 || txtrType == 2 || txtrType == 4) ? txtrType : RT_TEX_NONE;
+    m.texture = (txtrType == 1 || txtrType == 2 || txtrType == 3 || txtrType == 4 || txtrType == 6) ? txtrType : RT_TEX_NONE;
     m.tex_top = (txtrType == 1 && txTop) ? texTop : -1;
     m.use_photon_map = photonMap;
     m.caustic_photons = caustic;
@@ -80,7 +109,7 @@ struct CliLoader {
     m.k_trans = kTrans;
     m.perm = rfrIdx;
     m.perm_clr[0] = permClr.r; m.perm_clr[1] = permClr.g; m.perm_clr[2] = permClr.b;
-    if (txtrType == 2 || txtrType == 4) {
+    if (txtrType == 2 || txtrType == 3 || txtrType == 4 || txtrType == 6) {
       m.noise_scale = noiseScale; m.turb_mult = turbMult; m.color_scale = colorScale; m.color_mult = colorMult;
       m.period_mult[0] = pdMult.x; m.period_mult[1] = pdMult.y; m.period_mult[2] = pdMult.z;
       m.octaves = octaves; m.rnd_colors = rndColors; m.use_fwd_trans = useFwdTrans;
@@ -291,6 +320,30 @@ struct CliLoader {
             noiseScale = 1.0; turbMult = 15.0; colorScale = 24.0; colorMult = .1;
             pdMult = d3(TWO_PI_F * 0.1, TWO_PI_F * 31.4, TWO_PI_F * 4.1);
           }
+        } else if (c == "wood" || c == "wood2") {  // setTexture (myScene.java:717-742)
+          reset_dflt_txtr();
+          const bool w2 = c == "wood2";
+          txtrType = w2 ? RT_TEX_WOOD2 : RT_TEX_WOOD;
+          bool dflt = read_perlin(t);
+          if (!useCustClrs) {
+            if (w2) { colors[0] = clr(0.3, 0.20, 0.16); colors[1] = clr(0.94, 0.8, 0.4); }    // clr_dkwood2, clr_ltwood2
+            else { colors[0] = clr(0.2, 0.08, 0.08); colors[1] = clr(0.94, 0.47, 0.12); }     // clr_dkwood1, clr_ltwood1
+          }
+          if (dflt) {
+            octaves = w2 ? 8 : 4; rndColors = true; useFwdTrans = false;
+            noiseScale = w2 ? 1.0 : 2.0; turbMult = .4; colorScale = 25.0; colorMult = w2 ? .3 : .2;
+            pdMult = w2 ? d3(TWO_PI_F * 3.5, 7.9, 6.2) : d3(TWO_PI_F * 2.7, 3.6, 4.3);
+          }
+        } else if (c == "noise_color") {  // setTxtrColor (myScene.java:604-640)
+          if (!useCustClrs) { useCustClrs = true; ncust = 0; colors[0] = colors[1] = clr(1, 1, 1); }
+          Clr col;
+          if (t.at(1) == "named") {
+            if (!named_color(t.at(2), col)) { err = "unknown colour name: " + t.at(2); return false; }
+          } else {
+            col = clr(num(t, 1), num(t, 2), num(t, 3));
+          }
+          if (ncust < 2) colors[ncust] = col;  // the Perlin textures use the first two
+          ncust++;
         } else if (c == "begin") {  // :290-295
           poly = new_prim((t.size() > 1 && t[1] == "quad") ? RT_PRIM_QUAD : RT_PRIM_TRIANGLE);
           poly.nverts = poly.type == RT_PRIM_QUAD ? 4 : 3;

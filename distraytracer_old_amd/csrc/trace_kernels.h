@@ -455,6 +455,23 @@ DEVI V image_color(const SceneD& S, const HitRec& h, const Key& k, const TexD& T
   return lerpc(c0, fv, c1);
 }
 
+// myNoiseTexture.getClrAra (myTextureHandler.java:277-294): colours 0 and 1 interpolated by
+// distVal, each channel scaled by float noise of the permuted, colorScale-scaled point
+DEVI V clr_ara(const MatD& m, double distVal, V raw) {
+  V pt = mk(raw.x * m.colorScale, raw.y * m.colorScale, raw.z * m.colorScale);
+  double rm0 = 1.0, rm1 = 1.0, rm2 = 1.0;
+  if (m.rndColors) {
+    rm0 = 1.0 + (m.colorMult * noise3((float)pt.x, (float)pt.z, (float)pt.y));
+    rm1 = 1.0 + (m.colorMult * noise3((float)pt.y, (float)pt.x, (float)pt.z));
+    rm2 = 1.0 + (m.colorMult * noise3((float)pt.z, (float)pt.y, (float)pt.x));
+  }
+  const double* c0 = m.colors[0];
+  const double* c1 = m.colors[1];
+  return mk(jmax(0, jmin(1.0, (c0[0]) + rm0 * distVal * ((c1[0]) - (c0[0])))),
+            jmax(0, jmin(1.0, (c0[1]) + rm1 * distVal * ((c1[1]) - (c0[1])))),
+            jmax(0, jmin(1.0, (c0[2]) + rm2 * distVal * ((c1[2]) - (c0[2])))));
+}
+
 // getDiffTxtrColor of the shader's texture handler (myTextureHandler.java)
 template <bool CNT, uint32_t F>
 DEVI V diff_color(const SceneD& S, const MatD& m, const HitRec& h, const Key& k, double diffConst, Counters& ct) {
@@ -463,15 +480,15 @@ DEVI V diff_color(const SceneD& S, const MatD& m, const HitRec& h, const Key& k,
       V c = (m.texTop >= 0) ? image_color<CNT>(S, h, k, S.tex[m.texTop], ct) : ld3(m.diffuse);
       return mk(c.x * diffConst, c.y * diffConst, c.z * diffConst);
     }
-    if (m.tex == 2 || m.tex == 4) {
+    if (m.tex == 2 || m.tex == 3 || m.tex == 4 || m.tex == 6) {
       V hv = m.useFwdTrans ? h.fwd : h.hitLoc;
-      hv = mk(hv.x * m.scale, hv.y * m.scale, hv.z * m.scale);
+      hv = mk(hv.x * m.scale, hv.y * m.scale, hv.z * m.scale);  // getNoiseVal / getTurbVal scale hitVal in place
       V out;
       if (m.tex == 2) {  // myNoiseTexture :257-265
         double res = m.turbMult * noise3((float)hv.x, (float)hv.y, (float)hv.z);
         double val = .5 * res + .5;
         out = mk(val, val, val);
-      } else {  // myMarbleTexture :366-377 with getAbsTurbVal :242-251 and getClrAra :277-294
+      } else if (m.tex == 4) {  // myMarbleTexture :366-377 with getAbsTurbVal :242-251
         double res = 0, fs = 1.0, as = 1.0;
         for (int i = 0; i < m.octaves; ++i) {
           res += fabs(noise3((float)(hv.x * fs), (float)(hv.y * fs), (float)(hv.z * fs))) * as;
@@ -481,18 +498,32 @@ DEVI V diff_color(const SceneD& S, const MatD& m, const HitRec& h, const Key& k,
         double lin = (hv.x * m.periodMult[0] + hv.y * m.periodMult[1] + hv.z * m.periodMult[2]);
         double spt = lin / m.pmMag + m.turbMult * res;
         double dv = .5 * sin(spt) + .5;
-        V pt = mk(hv.x * m.colorScale, hv.y * m.colorScale, hv.z * m.colorScale);
-        double rm0 = 1.0, rm1 = 1.0, rm2 = 1.0;
-        if (m.rndColors) {
-          rm0 = 1.0 + (m.colorMult * noise3((float)pt.x, (float)pt.z, (float)pt.y));
-          rm1 = 1.0 + (m.colorMult * noise3((float)pt.y, (float)pt.x, (float)pt.z));
-          rm2 = 1.0 + (m.colorMult * noise3((float)pt.z, (float)pt.y, (float)pt.x));
+        out = clr_ara(m, dv, hv);
+      } else {  // wood: sqPtVal (myTextureHandler.java:275) + turbulence, banded by sin
+        const double* pm = m.periodMult;
+        double res;
+        if (m.tex == 3) {  // myBaseWoodTexture :309-331: one noise octave
+          res = noise3((float)hv.x, (float)hv.y, (float)hv.z);
+        } else {  // myWoodTexture :334-356 with getTurbVal :225-233
+          res = 0;
+          double fs = 1.0, as = 1.0;
+          for (int i = 0; i < m.octaves; ++i) {
+            res += noise3((float)(hv.x * fs), (float)(hv.y * fs), (float)(hv.z * fs)) * as;
+            as *= .5;
+            fs *= 1.92;
+          }
         }
-        const double* c0 = m.colors[0];
-        const double* c1 = m.colors[1];
-        out = mk(jmax(0, jmin(1.0, (c0[0]) + rm0 * dv * ((c1[0]) - (c0[0])))),
-                 jmax(0, jmin(1.0, (c0[1]) + rm1 * dv * ((c1[1]) - (c0[1])))),
-                 jmax(0, jmin(1.0, (c0[2]) + rm2 * dv * ((c1[2]) - (c0[2])))));
+        const double sq = sqrt((hv.x * hv.x) * pm[0] + (hv.y * hv.y) * pm[1] + (hv.z * hv.z) * pm[2]) + m.turbMult * res;
+        double dv = sin(sq * m.pmMag);
+        if (m.tex == 3) {
+          dv *= 1.1;
+          dv += .5;
+          dv = (dv < 0 ? 0 : (dv > 1 ? 1 : dv));
+          out = clr_ara(m, dv, h.hitLoc);  // base wood: colours from the unscaled object-space hit
+        } else {
+          dv = 1 - (dv < 0 ? 0 : dv);
+          out = clr_ara(m, dv, hv);
+        }
       }
       if (fabs(diffConst - 1.0) > EPS) out = mk(out.x * diffConst, out.y * diffConst, out.z * diffConst);
       return out;

@@ -231,7 +231,7 @@ struct BBox : GeomBase {
 
 // ---------------------------------------------------------------------------
 // shaders (myObjShader.java)
-enum TexKind { TX_NONE = 0, TX_IMAGE = 1, TX_NOISE = 2, TX_MARBLE = 4 };
+enum TexKind { TX_NONE = 0, TX_IMAGE = 1, TX_NOISE = 2, TX_WOOD = 3, TX_MARBLE = 4, TX_WOOD2 = 6 };
 struct Shader {
   bool simple = false;  // mySimpleReflObjShdr
   Color diffuse, ambient, specular, curPermClr, KReflClr;
@@ -1017,6 +1017,37 @@ static void clr_ara(const Shader* sh, double distVal, const V3& raw, double res[
   res[1] = jmax(0, jmin(1.0, (c0.g) + rm[1] * distVal * ((c1.g) - (c0.g))));
   res[2] = jmax(0, jmin(1.0, (c0.b) + rm[2] * distVal * ((c1.b) - (c0.b))));
 }
+// DistRayTracer.getClr (DistRayTracer.java:467-530): the named colours of noise_color
+// (clr_rnd draws from Processing's unseeded random and is not supported)
+static bool named_color(std::string n, Color& c) {
+  for (auto& ch : n) ch = (char)std::tolower(ch);
+  static const std::map<std::string, V3> tab = {
+      {"clr_gray", V3(0.47, 0.47, 0.47)}, {"clr_white", V3(1.0, 1.0, 1.0)}, {"clr_yellow", V3(1.0, 1.0, 0)},
+      {"clr_cyan", V3(0, 1.0, 1.0)}, {"clr_magenta", V3(1.0, 0, 1.0)}, {"clr_red", V3(1.0, 0, 0)},
+      {"clr_blue", V3(0, 0, 1.0)}, {"clr_purple", V3(0.6, 0.2, 1.0)}, {"clr_green", V3(0, 1.0, 0)},
+      {"clr_ltwood1", V3(0.94, 0.47, 0.12)}, {"clr_ltwood2", V3(0.94, 0.8, 0.4)}, {"clr_dkwood1", V3(0.2, 0.08, 0.08)},
+      {"clr_dkwood2", V3(0.3, 0.20, 0.16)}, {"clr_mortar1", V3(0.2, 0.2, 0.2)}, {"clr_mortar2", V3(0.7, 0.7, 0.7)},
+      {"clr_brick1_1", V3(0.6, 0.18, 0.22)}, {"clr_brick1_2", V3(0.8, 0.26, 0.33)}, {"clr_brick2_1", V3(0.6, 0.32, 0.16)},
+      {"clr_brick2_2", V3(0.8, 0.45, 0.25)}, {"clr_brick3_1", V3(0.3, 0.01, 0.07)}, {"clr_brick3_2", V3(0.6, 0.02, 0.13)},
+      {"clr_brick4_1", V3(0.4, 0.1, 0.17)}, {"clr_brick4_2", V3(0.6, 0.3, 0.13)}, {"clr_darkgray", V3(0.31, 0.31, 0.31)},
+      {"clr_darkred", V3(0.47, 0, 0)}, {"clr_darkblue", V3(0, 0, 0.47)}, {"clr_darkpurple", V3(0.4, 0.2, 0.6)},
+      {"clr_darkgreen", V3(0, 0.47, 0)}, {"clr_darkyellow", V3(0.47, 0.47, 0)}, {"clr_darkmagenta", V3(0.47, 0, 0.47)},
+      {"clr_darkcyan", V3(0, 0.47, 0.47)}, {"clr_lightgray", V3(0.78, 0.78, 0.78)}, {"clr_lightred", V3(1.0, .43, .43)},
+      {"clr_lightblue", V3(0.43, 0.43, 1.0)}, {"clr_lightgreen", V3(0.43, 1.0, 0.43)}, {"clr_lightyellow", V3(1.0, 1.0, .43)},
+      {"clr_lightmagenta", V3(1.0, .43, 1.0)}, {"clr_lightcyan", V3(0.43, 1.0, 1.0)}, {"clr_black", V3(0, 0, 0)},
+      {"clr_nearblack", V3(0.05, 0.05, 0.05)}, {"clr_faintgray", V3(0.43, 0.43, 0.43)}, {"clr_faintred", V3(0.43, 0, 0)},
+      {"clr_faintblue", V3(0, 0, 0.43)}, {"clr_faintgreen", V3(0, 0.43, 0)}, {"clr_faintyellow", V3(0.43, 0.43, 0)},
+      {"clr_faintcyan", V3(0, 0.43, 0.43)}, {"clr_faintmagenta", V3(0.43, 0, 0.43)}, {"clr_offwhite", V3(0.95, 0.98, 0.92)}};
+  auto it = tab.find(n);
+  if (it == tab.end()) {
+    if (n == "clr_rnd") return false;
+    c = Color(1.0, 1.0, 1.0);  // "Color not found ... so using white"
+    return true;
+  }
+  c = Color(it->second.x, it->second.y, it->second.z);
+  return true;
+}
+
 static void diff_txtr_color(Shader* sh, Hit& hit, double diffConst, double out[3], uint64_t* st) {
   if (sh->tex == TX_IMAGE) {  // myImageTexture.getDiffTxtrColor :105-117
     if (sh->txTop && sh->texTop) image_color(hit, *sh->texTop, out, st);
@@ -1024,9 +1055,31 @@ static void diff_txtr_color(Shader* sh, Hit& hit, double diffConst, double out[3
     out[0] *= diffConst; out[1] *= diffConst; out[2] *= diffConst;
     return;
   }
-  if (sh->tex == TX_NOISE || sh->tex == TX_MARBLE) {
+  if (sh->tex == TX_NOISE || sh->tex == TX_MARBLE || sh->tex == TX_WOOD || sh->tex == TX_WOOD2) {
     V3 hv = sh->useFwdTrans ? hit.fwdTransHitLoc : hit.hitLoc;
-    if (sh->tex == TX_NOISE) {  // myNoiseTexture :257-265
+    const V3& pm = sh->periodMult;
+    if (sh->tex == TX_WOOD) {  // myBaseWoodTexture (myTextureHandler.java:309-331); getNoiseVal scales hitVal in place
+      hv = V3(hv.x * sh->scale, hv.y * sh->scale, hv.z * sh->scale);
+      double res = noise3((float)hv.x, (float)hv.y, (float)hv.z);
+      double sq = std::sqrt((hv.x * hv.x) * pm.x + (hv.y * hv.y) * pm.y + (hv.z * hv.z) * pm.z) + sh->turbMult * res;
+      double distVal = std::sin(sq * mag(pm));
+      distVal *= 1.1;
+      distVal += .5;
+      distVal = (distVal < 0 ? 0 : (distVal > 1 ? 1 : distVal));
+      clr_ara(sh, distVal, hit.hitLoc, out);  // the base wood colours from the unscaled object-space hit
+    } else if (sh->tex == TX_WOOD2) {  // myWoodTexture (:334-356) with getTurbVal (:225-233)
+      hv = V3(hv.x * sh->scale, hv.y * sh->scale, hv.z * sh->scale);
+      double res = 0, fs = 1.0, as = 1.0;
+      for (int i = 0; i < sh->numOctaves; ++i) {
+        res += noise3((float)(hv.x * fs), (float)(hv.y * fs), (float)(hv.z * fs)) * as;
+        as *= .5;
+        fs *= 1.92;
+      }
+      double sq = std::sqrt((hv.x * hv.x) * pm.x + (hv.y * hv.y) * pm.y + (hv.z * hv.z) * pm.z) + sh->turbMult * res;
+      double distVal = (std::sin(sq * mag(pm)));
+      distVal = 1 - (distVal < 0 ? 0 : distVal);
+      clr_ara(sh, distVal, hv, out);
+    } else if (sh->tex == TX_NOISE) {  // myNoiseTexture :257-265
       hv = V3(hv.x * sh->scale, hv.y * sh->scale, hv.z * sh->scale);
       double res = sh->turbMult * noise3((float)hv.x, (float)hv.y, (float)hv.z);
       double val = .5 * res + .5;
@@ -1466,7 +1519,7 @@ struct Loader {
     sh->isCausticPhtn = s->isCausticPhtn;
     sh->diffConst = 1 - rfrIdx;
     sh->phongExp = phong;
-    sh->tex = (txtrType == 1 || txtrType == 2 || txtrType == 4) ? txtrType : TX_NONE;
+    sh->tex = (txtrType == 1 || txtrType == 2 || txtrType == 3 || txtrType == 4 || txtrType == 6) ? txtrType : TX_NONE;
     if (txtrType == 1) {
       sh->txTop = txTop;
       if (txTop) {
@@ -1475,7 +1528,8 @@ struct Loader {
         else sh->texTop = &it->second;
       }
     }
-    if (txtrType == 2 || txtrType == 4) {
+    if (txtrType == 2 || txtrType == 3 || txtrType == 4 || txtrType == 6) {
+      while (noiseColors.size() < 2) noiseColors.push_back(Color(1, 1, 1));  // (Java would throw at render)
       sh->scale = noiseScale; sh->numOctaves = numOctaves; sh->turbMult = turbMult; sh->periodMult = pdMult;
       sh->colorScale = colorScale; sh->colorMult = colorMult; sh->rndColors = rndColors; sh->useFwdTrans = useFwdTrans;
       sh->colors = noiseColors;
@@ -1690,8 +1744,30 @@ struct Loader {
             noiseScale = 1.0; turbMult = 15.0; colorScale = 24.0; colorMult = .1;
             pdMult = V3(TWO_PI_F * 0.1, TWO_PI_F * 31.4, TWO_PI_F * 4.1);
           }
-        } else if (c == "wood" || c == "wood2" || c == "stone" || c == "noise_color") {
-          err = "unsupported texture command (out of hot-path scope): " + c;
+        } else if (c == "wood" || c == "wood2") {  // setTexture (myScene.java:717-742)
+          reset_dflt_txtr();
+          const bool w2 = c == "wood2";
+          txtrType = w2 ? 6 : 3;
+          bool dflt = read_perlin(t);
+          if (!useCustClrs)
+            noiseColors = w2 ? std::vector<Color>{Color(0.3, 0.20, 0.16), Color(0.94, 0.8, 0.4)}      // clr_dkwood2, clr_ltwood2
+                             : std::vector<Color>{Color(0.2, 0.08, 0.08), Color(0.94, 0.47, 0.12)};  // clr_dkwood1, clr_ltwood1
+          if (dflt) {
+            numOctaves = w2 ? 8 : 4; rndColors = true; useFwdTrans = false;
+            noiseScale = w2 ? 1.0 : 2.0; turbMult = .4; colorScale = 25.0; colorMult = w2 ? .3 : .2;
+            pdMult = w2 ? V3(TWO_PI_F * 3.5, 7.9, 6.2) : V3(TWO_PI_F * 2.7, 3.6, 4.3);
+          }
+        } else if (c == "noise_color") {  // setTxtrColor (myScene.java:604-640); weights are unused by these textures
+          if (!useCustClrs) { noiseColors.clear(); useCustClrs = true; }
+          Color col;
+          if (t.at(1) == "named") {
+            if (!named_color(t.at(2), col)) { err = "unknown colour name: " + t.at(2); return false; }
+          } else {
+            col = Color(num(t, 1), num(t, 2), num(t, 3));
+          }
+          noiseColors.push_back(col);
+        } else if (c == "stone") {
+          err = "unsupported texture command (cellular texture, out of scope): " + c;
           return false;
         } else if (c == "begin") {
           vertType = t.size() > 1 ? t[1] : "triangle";

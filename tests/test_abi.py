@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(rt.EXPORTS)
-    assert L.rt_abi_version() == 1
+    assert L.rt_abi_version() == 2
 
 
 def test_no_gpu_fails_loudly():
@@ -63,8 +63,10 @@ def test_host_builder_matches_oracle_topology(cfg):
 
 
 @pytest.mark.parametrize("cli", ["p2_t03.cli", "p2_t05.cli", "p2_t07.cli", "c2clear.cli", "t05.cli", "p3_t05.cli",
-                                 "earth.cli", "cylinder1.cli"])
+                                 "earth.cli", "cylinder1.cli", "old_t07.cli", "old_t10.cli", "planets3Ortho.cli",
+                                 "p3_t09.cli", "p4_t05.cli", "p4_t06_2.cli"])
 def test_host_builder_feature_scenes(cli):
+    scenes.ensure_bun69k()
     tex = scenes.prepare(cli)
     a = rt.inspect_cli(cli, textures=tex)
     b = OracleScene(scenes.SCENE_DIR, cli, tex).info()

@@ -70,9 +70,12 @@ def test_camera_scenes_parity(cli, spp):
         assert (int(ag[0, 0]) & 0xFFFFFFFF) == 0xFF000000 and rg[0, 0].max() == 0
 
 
-@pytest.mark.parametrize("cli,spp", [("p2_t05.cli", 4), ("p2_t07.cli", 4), ("c2clear.cli", 1), ("p2_t03.cli", 4)])
+@pytest.mark.parametrize("cli,spp", [("p2_t05.cli", 4), ("p2_t07.cli", 4), ("c2clear.cli", 1), ("p2_t03.cli", 4),
+                                     ("p3_t09.cli", 2), ("p4_t05.cli", 2), ("p4_t06_2.cli", 2)])
 def test_feature_scenes_parity(cli, spp):
-    """disk light (p2_t05), depth of field (p2_t07), refraction (c2clear), motion blur (p2_t03)."""
+    """disk light (p2_t05), depth of field (p2_t07), refraction (c2clear), motion blur (p2_t03),
+    procedural wood (p3_t09 = C3 with its wood line; myBaseWoodTexture), wood2 with named
+    noise_color (p4_t05; myWoodTexture) and marble with custom noise_color (p4_t06_2)."""
     g, o, (rg, ag), (ro, ao) = both(cli, 128, 128, spp)
     c = compare(rg, ag, ro, ao)
     assert c["mismatch_frac"] < 2e-3, c
