@@ -15,6 +15,7 @@ int set_error(int code, const std::string& msg);
 struct HostScene {
   std::vector<XformD> xf;
   std::vector<TriD> tri;
+  std::vector<double> triUV;  // texture_coord of the 3 vertices (file order), 6 per triangle
   std::vector<PrimD> prim;
   std::vector<NodeD> node;
   std::vector<LeafD> leaf;

@@ -115,6 +115,7 @@ static constexpr int PHOTON_LEAF = 24;
 struct SceneD {
   const XformD* xf;
   const TriD* tri;
+  const double* triUV;  // [ntri][3][2] texture_coord, nullptr when no triangle is image-textured
   const PrimD* prim;
   const NodeD* node;
   const LeafD* leaf;

@@ -124,6 +124,7 @@ struct Builder {
         t.dA = A.D; t.dB = B.D;
         t.xf = xf; t.xfc = -1; t.mat = p.material; t.key = (uint32_t)i;
         hs.tri.push_back(t);
+        for (int k = 0; k < 3; ++k) { hs.triUV.push_back(p.uv[k][0]); hs.triUV.push_back(p.uv[k][1]); }
         ref[i] = (int32_t)hs.tri.size() - 1;
       } else {
         PrimD q;
@@ -457,8 +458,13 @@ void pack_leaves(HostScene& hs) {
   for (int r = 0; r < nt; ++r)
     if (perm[r] < 0) { perm[r] = (int32_t)order.size(); order.push_back(r); }
   std::vector<TriD> tri(nt);
-  for (int k = 0; k < nt; ++k) tri[k] = hs.tri[order[k]];
+  std::vector<double> uv(hs.triUV.size());
+  for (int k = 0; k < nt; ++k) {
+    tri[k] = hs.tri[order[k]];
+    if (!uv.empty()) std::memcpy(&uv[6 * (size_t)k], &hs.triUV[6 * (size_t)order[k]], 6 * sizeof(double));
+  }
   hs.tri.swap(tri);
+  hs.triUV.swap(uv);
   for (int32_t& r : hs.member)
     if (r >= 0) r = perm[r];
   for (TopD& t : hs.top)

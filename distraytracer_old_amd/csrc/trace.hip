@@ -60,6 +60,12 @@ static int upload_scene(rt_scene* s) {
       (rc = upload(s, h.accel, &d.accel)) || (rc = upload(s, h.top, &d.top)) || (rc = upload(s, h.mat, &d.mat)) ||
       (rc = upload(s, h.light, &d.light)) || (rc = upload(s, h.tex, &d.tex)) || (rc = upload(s, h.texel, &d.texel)))
     return rc;
+  d.triUV = nullptr;
+  {  // triangle UVs only matter for image-textured triangles
+    bool need = false;
+    for (const TriD& t : h.tri) need = need || h.mat[t.mat].tex == RT_TEX_IMAGE;
+    if (need && (rc = upload(s, h.triUV, &d.triUV))) return rc;
+  }
   d.ntop = (int)h.top.size();
   d.nlight = (int)h.light.size();
   d.pnode = nullptr;

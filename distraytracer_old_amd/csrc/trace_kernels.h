@@ -421,7 +421,12 @@ DEVI V image_color(const SceneD& S, const HitRec& h, const Key& k, const TexD& T
     int nv = 3;
     if (h.type == PT_TRI) {
       const TriD& T3 = S.tri[h.ref];
-      for (int i = 0; i < 3; ++i) { for (int c = 0; c < 3; ++c) vx[i][c] = T3.v[i][c]; uvv[i][0] = 0; uvv[i][1] = 0; }
+      const double* tuv = S.triUV ? S.triUV + 6 * (size_t)h.ref : nullptr;
+      for (int i = 0; i < 3; ++i) {
+        for (int c = 0; c < 3; ++c) vx[i][c] = T3.v[i][c];
+        uvv[i][0] = tuv ? tuv[2 * i] : 0;
+        uvv[i][1] = tuv ? tuv[2 * i + 1] : 0;
+      }
     } else {
       const PrimD& P = S.prim[~h.ref];
       nv = 4;
