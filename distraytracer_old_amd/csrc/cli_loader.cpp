@@ -5,8 +5,8 @@
 // stack). It emits the flattened rt_scene_desc that a JNI myScene subclass
 // would hand over, then calls rt_scene_create().
 //
-// Commands outside the hot-path scope (instances, sierpinski, the cellular
-// `stone` texture) are rejected with RT_E_PARSE.
+// Commands outside the hot-path scope (instances, sierpinski) are rejected
+// with RT_E_PARSE.
 #include <cctype>
 #include <fstream>
 #include <map>
@@ -70,8 +70,9 @@ struct CliLoader {
   int octaves = 8;
   D3 pdMult{10, 10, 10};
   bool rndColors = false, useFwdTrans = false, useCustClrs = false;
-  Clr colors[2] = {clr(.7, .7, .7), clr(.2, .2, .2)};
-  int ncust = 0;  // noise_color entries since the last reset
+  std::vector<Clr> noiseColors{clr(.7, .7, .7), clr(.2, .2, .2)};
+  int numPtsDist = 2, distFunc = 1, roiFunc = 1;
+  double avgNumPerCell = 1.0, mortarThresh = 0.05;
   bool photonMap = false, caustic = false;
   // accumulated desc
   std::vector<rt_prim_desc> prims;
@@ -96,7 +97,7 @@ struct CliLoader {
     rt_material_desc m;
     std::memset(&m, 0, sizeof(m));
     m.simple = simple;
-    m.texture = (txtrType == 1 || txtrType == 2 || txtrType == 3 || txtrType == 4 || txtrType == 6) ? txtrType : RT_TEX_NONE;
+    m.texture = (txtrType >= 1 && txtrType <= 6) ? txtrType : RT_TEX_NONE;
     m.tex_top = (txtrType == 1 && txTop) ? texTop : -1;
     m.use_photon_map = photonMap;
     m.caustic_photons = caustic;
@@ -109,11 +110,18 @@ struct CliLoader {
     m.k_trans = kTrans;
     m.perm = rfrIdx;
     m.perm_clr[0] = permClr.r; m.perm_clr[1] = permClr.g; m.perm_clr[2] = permClr.b;
-    if (txtrType == 2 || txtrType == 3 || txtrType == 4 || txtrType == 6) {
+    if (txtrType >= 2 && txtrType <= 6) {
       m.noise_scale = noiseScale; m.turb_mult = turbMult; m.color_scale = colorScale; m.color_mult = colorMult;
       m.period_mult[0] = pdMult.x; m.period_mult[1] = pdMult.y; m.period_mult[2] = pdMult.z;
       m.octaves = octaves; m.rnd_colors = rndColors; m.use_fwd_trans = useFwdTrans;
-      for (int i = 0; i < 2; ++i) { m.colors[i][0] = colors[i].r; m.colors[i][1] = colors[i].g; m.colors[i][2] = colors[i].b; }
+      std::vector<Clr> cl = noiseColors;
+      while (cl.size() < 2) cl.push_back(clr(1, 1, 1));  // (Java would throw at render)
+      m.num_colors = (int32_t)std::min<size_t>(cl.size(), RT_MAX_NOISE_COLORS);
+      for (int i = 0; i < m.num_colors; ++i) { m.colors[i][0] = cl[i].r; m.colors[i][1] = cl[i].g; m.colors[i][2] = cl[i].b; }
+      if (txtrType == RT_TEX_STONE) {
+        m.dist_func = distFunc; m.roi_func = roiFunc; m.num_pts_dist = numPtsDist;
+        m.avg_per_cell = avgNumPerCell; m.mortar_thresh = mortarThresh;
+      }
     }
     for (size_t i = 0; i < mats.size(); ++i)
       if (std::memcmp(&mats[i], &m, sizeof(m)) == 0) return (int)i;
@@ -138,7 +146,28 @@ struct CliLoader {
     txtrType = 0; octaves = 4; rndColors = false; useCustClrs = false; useFwdTrans = false;
     noiseScale = 1.0; turbMult = 1.0; colorScale = 5.0; colorMult = .1;
     pdMult = d3(1.0, 1.0, 1.0);
-    colors[0] = clr(0.05, 0.05, 0.05); colors[1] = clr(1.0, 1.0, 1.0);
+    noiseColors = {clr(0.05, 0.05, 0.05), clr(1.0, 1.0, 1.0)};
+    numPtsDist = 2; distFunc = 1; roiFunc = 1; avgNumPerCell = 1.0; mortarThresh = 0.05;
+  }
+  bool read_worley(const std::vector<std::string>& v) {  // readProcTxtrWorleyVals (myScene.java:675-708)
+    try {
+      size_t k = 1;
+      noiseScale = num(v, k++);
+      distFunc = std::stoi(v.at(k++));
+      roiFunc = std::stoi(v.at(k++));
+      numPtsDist = std::stoi(v.at(k++));
+      avgNumPerCell = num(v, k++);
+      mortarThresh = num(v, k++);
+      useFwdTrans = (num(v, k++) == 1.0);
+      if (v.size() >= k + 2) {
+        colorScale = num(v, k); colorMult = num(v, k + 1); rndColors = true;
+      } else {
+        rndColors = false; colorScale = 25.0; colorMult = .1;
+      }
+      return false;
+    } catch (...) {
+      return true;
+    }
   }
   static double num(const std::vector<std::string>& t, size_t i) {
     if (i >= t.size()) throw std::out_of_range("missing argument");
@@ -314,7 +343,7 @@ struct CliLoader {
           reset_dflt_txtr();
           txtrType = 4;
           bool dflt = read_perlin(t);
-          if (!useCustClrs) { colors[0] = clr(0.05, 0.05, 0.05); colors[1] = clr(0.95, 0.98, 0.92); }
+          if (!useCustClrs) noiseColors = {clr(0.05, 0.05, 0.05), clr(0.95, 0.98, 0.92)};
           if (dflt) {
             octaves = 16; rndColors = true; useFwdTrans = false;
             noiseScale = 1.0; turbMult = 15.0; colorScale = 24.0; colorMult = .1;
@@ -326,8 +355,8 @@ struct CliLoader {
           txtrType = w2 ? RT_TEX_WOOD2 : RT_TEX_WOOD;
           bool dflt = read_perlin(t);
           if (!useCustClrs) {
-            if (w2) { colors[0] = clr(0.3, 0.20, 0.16); colors[1] = clr(0.94, 0.8, 0.4); }    // clr_dkwood2, clr_ltwood2
-            else { colors[0] = clr(0.2, 0.08, 0.08); colors[1] = clr(0.94, 0.47, 0.12); }     // clr_dkwood1, clr_ltwood1
+            noiseColors = w2 ? std::vector<Clr>{clr(0.3, 0.20, 0.16), clr(0.94, 0.8, 0.4)}      // clr_dkwood2, clr_ltwood2
+                             : std::vector<Clr>{clr(0.2, 0.08, 0.08), clr(0.94, 0.47, 0.12)};  // clr_dkwood1, clr_ltwood1
           }
           if (dflt) {
             octaves = w2 ? 8 : 4; rndColors = true; useFwdTrans = false;
@@ -335,15 +364,27 @@ struct CliLoader {
             pdMult = w2 ? d3(TWO_PI_F * 3.5, 7.9, 6.2) : d3(TWO_PI_F * 2.7, 3.6, 4.3);
           }
         } else if (c == "noise_color") {  // setTxtrColor (myScene.java:604-640)
-          if (!useCustClrs) { useCustClrs = true; ncust = 0; colors[0] = colors[1] = clr(1, 1, 1); }
+          if (!useCustClrs) { useCustClrs = true; noiseColors.clear(); }
           Clr col;
           if (t.at(1) == "named") {
             if (!named_color(t.at(2), col)) { err = "unknown colour name: " + t.at(2); return false; }
           } else {
             col = clr(num(t, 1), num(t, 2), num(t, 3));
           }
-          if (ncust < 2) colors[ncust] = col;  // the Perlin textures use the first two
-          ncust++;
+          noiseColors.push_back(col);
+        } else if (c == "stone") {  // setTexture (myScene.java:756-771): myCellularTexture
+          reset_dflt_txtr();
+          txtrType = RT_TEX_STONE;
+          bool dflt = read_worley(t);
+          if (!useCustClrs)
+            noiseColors = {clr(0.2, 0.2, 0.2), clr(0.7, 0.7, 0.7), clr(0.6, 0.18, 0.22), clr(0.8, 0.26, 0.33),
+                           clr(0.6, 0.32, 0.16), clr(0.8, 0.45, 0.25), clr(0.3, 0.01, 0.07), clr(0.6, 0.02, 0.13),
+                           clr(0.4, 0.1, 0.17), clr(0.6, 0.3, 0.13)};  // clr_mortar1/2, clr_brick1_1 .. clr_brick4_2
+          if (dflt) {
+            octaves = 8; numPtsDist = 2; distFunc = 1; roiFunc = 1; rndColors = true; useFwdTrans = false;
+            noiseScale = 4.0; turbMult = 1.0; colorScale = 12.0; colorMult = .2; avgNumPerCell = 1.0; mortarThresh = 0.05;
+            pdMult = d3(10.0, 10.0, 10.0);
+          }
         } else if (c == "begin") {  // :290-295
           poly = new_prim((t.size() > 1 && t[1] == "quad") ? RT_PRIM_QUAD : RT_PRIM_TRIANGLE);
           poly.nverts = poly.type == RT_PRIM_QUAD ? 4 : 3;

@@ -83,7 +83,11 @@ struct MatD {
   // noise / marble
   double scale, turbMult, colorScale, colorMult, pmMag;
   double periodMult[3];
-  double colors[2][3];
+  double colors[16][3];  // RT_MAX_NOISE_COLORS
+  // myCellularTexture: Poisson point-count table (cumulative probability keys, ascending)
+  double mortar, pdfKey[14];
+  int32_t pdfVal[14], npdf, ncolors;
+  int32_t distFunc, roiFunc, numPtsDist, pad0;
   int32_t simple, hasCaustic, usePhotonMap, isCausticPhtn;
   int32_t tex, texTop, octaves, rndColors;
   int32_t useFwdTrans, pad[3];

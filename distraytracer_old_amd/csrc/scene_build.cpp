@@ -9,6 +9,7 @@
 //    endIDX = N-1 (Q1: last element of the root's split-axis order dropped)
 //    (myScene.java:312-318, myGeomBase.java:338-386, DistRayTracer.java:409-418).
 #include <algorithm>
+#include <cmath>
 #include <map>
 #include <string>
 
@@ -371,7 +372,6 @@ struct Builder {
       for (int c = 0; c < 3; ++c) {
         md.diffuse[c] = s.diffuse[c]; md.ambient[c] = s.ambient[c]; md.specular[c] = s.specular[c];
         md.kreflclr[c] = s.k_refl_clr[c]; md.permclr[c] = s.perm_clr[c]; md.periodMult[c] = s.period_mult[c];
-        md.colors[0][c] = s.colors[0][c]; md.colors[1][c] = s.colors[1][c];
       }
       md.avgDiffClr = (1.0 / 3.0) * (s.diffuse[0] + s.diffuse[1] + s.diffuse[2]);
       if (md.avgDiffClr != 0)
@@ -389,6 +389,26 @@ struct Builder {
       md.pmMag = std::sqrt(((s.period_mult[0] * s.period_mult[0]) + (s.period_mult[1] * s.period_mult[1])) +
                            (s.period_mult[2] * s.period_mult[2]));
       md.octaves = s.octaves; md.rndColors = s.rnd_colors; md.useFwdTrans = s.use_fwd_trans;
+      if (md.tex >= RT_TEX_NOISE && md.tex <= RT_TEX_WOOD2) {
+        if (s.num_colors < 2 || s.num_colors > RT_MAX_NOISE_COLORS) { err = "bad noise colour count"; return false; }
+        md.ncolors = s.num_colors;
+        for (int k = 0; k < s.num_colors; ++k)
+          for (int c = 0; c < 3; ++c) md.colors[k][c] = s.colors[k][c];
+      }
+      if (md.tex == RT_TEX_STONE) {  // myCellularTexture ctor (myTextureHandler.java:390-425)
+        if (s.num_pts_dist > 8) { err = "stone: more than 8 ROI points unsupported"; return false; }
+        if (s.num_colors < 4) { err = "stone: needs at least 4 noise colours (mortar pair + a brick pair)"; return false; }
+        md.distFunc = s.dist_func; md.roiFunc = s.roi_func; md.numPtsDist = s.num_pts_dist; md.mortar = s.mortar_thresh;
+        std::map<double, int> pdfs;  // ConcurrentSkipListMap: put replaces the value of an equal key
+        double lastDist = 1.0 / std::pow(M_E, s.avg_per_cell), cumProb = lastDist;
+        for (int i = 1; i < 15; ++i) {
+          lastDist *= (s.avg_per_cell / (1.0 * i));
+          cumProb += lastDist;
+          pdfs[cumProb] = i;
+        }
+        md.npdf = 0;
+        for (auto& e : pdfs) { md.pdfKey[md.npdf] = e.first; md.pdfVal[md.npdf] = e.second; md.npdf++; }
+      }
       hs.mat.push_back(md);
     }
     // lights (myLight.java:20-30, spot :150-157, disk :244-247)

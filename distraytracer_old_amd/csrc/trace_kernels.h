@@ -462,7 +462,7 @@ DEVI V image_color(const SceneD& S, const HitRec& h, const Key& k, const TexD& T
 
 // myNoiseTexture.getClrAra (myTextureHandler.java:277-294): colours 0 and 1 interpolated by
 // distVal, each channel scaled by float noise of the permuted, colorScale-scaled point
-DEVI V clr_ara(const MatD& m, double distVal, V raw) {
+DEVI V clr_ara(const MatD& m, double distVal, V raw, int i0 = 0, int i1 = 1) {
   V pt = mk(raw.x * m.colorScale, raw.y * m.colorScale, raw.z * m.colorScale);
   double rm0 = 1.0, rm1 = 1.0, rm2 = 1.0;
   if (m.rndColors) {
@@ -470,11 +470,109 @@ DEVI V clr_ara(const MatD& m, double distVal, V raw) {
     rm1 = 1.0 + (m.colorMult * noise3((float)pt.y, (float)pt.x, (float)pt.z));
     rm2 = 1.0 + (m.colorMult * noise3((float)pt.z, (float)pt.y, (float)pt.x));
   }
-  const double* c0 = m.colors[0];
-  const double* c1 = m.colors[1];
+  const double* c0 = m.colors[i0];
+  const double* c1 = m.colors[i1];
   return mk(jmax(0, jmin(1.0, (c0[0]) + rm0 * distVal * ((c1[0]) - (c0[0])))),
             jmax(0, jmin(1.0, (c0[1]) + rm1 * distVal * ((c1[1]) - (c0[1])))),
             jmax(0, jmin(1.0, (c0[2]) + rm2 * distVal * ((c1[2]) - (c0[2])))));
+}
+
+// java.util.Random as myCellularTexture uses it (new Random(hashInts(cell)), nextDouble)
+struct JRand {
+  uint64_t sd;
+  DEVI void seed(int32_t s) { sd = ((uint64_t)(int64_t)s ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1); }
+  DEVI int32_t next(int bits) {
+    sd = (sd * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+    return (int32_t)(int64_t)(sd >> (48 - bits));
+  }
+  DEVI double next_double() {
+    const int64_t hi = next(26);
+    return (double)((hi << 27) + next(27)) * 0x1.0p-53;
+  }
+};
+DEVI int32_t fastfloor(double x) { return x > 0 ? jd2i(x) : jd2i(x) - 1; }  // DistRayTracer.java:307
+DEVI int32_t hash_ints(int32_t x, int32_t y, int32_t z) {                    // DistRayTracer.hashInts (wraps)
+  return (int32_t)((uint32_t)x * 1572869u + (uint32_t)y * 6291469u + (uint32_t)z);
+}
+// myCellularTexture.getDiffTxtrColor (myTextureHandler.java:433-480): Worley points of the
+// 27 cells around the scaled hit (per-cell java.util.Random), the ROI function of the
+// smallest distinct distances, mortar below the threshold, else a brick colour pair drawn
+// from the nearest point's cell. The reference keeps every distance in a sorted map
+// (an equal distance replaces the cell); only the numPtsDist (<= 8) smallest are read, so
+// a sorted register list of 8 distinct distances gives the same keys and nearest cell.
+DEVI V cellular_color(const MatD& m, const HitRec& h) {
+  V hv = m.useFwdTrans ? h.fwd : h.hitLoc;
+  hv = mk(hv.x * m.scale, hv.y * m.scale, hv.z * m.scale);
+  const int32_t ix = fastfloor(hv.x), iy = fastfloor(hv.y), iz = fastfloor(hv.z);
+  constexpr int KD = 8;
+  double kd[KD];
+  int32_t kn[KD];
+#pragma unroll
+  for (int i = 0; i < KD; ++i) { kd[i] = INFINITY; kn[i] = 0; }
+  JRand rnd;
+  for (int n = 0; n < 27; ++n) {  // DistRayTracer.nghbrHdCells order (:21-25): x-major over {0,1,-1}
+    const int dx = (n / 9 == 2) ? -1 : n / 9, dy = ((n / 3) % 3 == 2) ? -1 : (n / 3) % 3, dz = (n % 3 == 2) ? -1 : n % 3;
+    const int32_t cx = ix + dx, cy = iy + dy, cz = iz + dz;
+    rnd.seed(hash_ints(cx, cy, cz));
+    const double prob = rnd.next_double();
+    int np = m.pdfVal[0];  // lowerKey(prob) (greatest key < prob), first entry when there is none
+    for (int j = 1; j < m.npdf; ++j)
+      if (m.pdfKey[j] < prob) np = m.pdfVal[j];
+    for (int j = 0; j < np; ++j) {
+      const double px = cx + rnd.next_double(), py = cy + rnd.next_double(), pz = cz + rnd.next_double();
+      const double d = (m.distFunc == 0)
+                           ? fabs(hv.x - px) + fabs(hv.y - py) + fabs(hv.z - pz)  // _L1Dist
+                           : sqrt(((hv.x - px) * (hv.x - px)) + ((hv.y - py) * (hv.y - py)) + ((hv.z - pz) * (hv.z - pz)));
+      bool eq = false;
+#pragma unroll
+      for (int i = 0; i < KD; ++i)
+        if (kd[i] == d) { kn[i] = n; eq = true; }
+      if (!eq && d < kd[KD - 1]) {  // sorted insert
+#pragma unroll
+        for (int i = KD - 1; i > 0; --i) {
+          if (kd[i - 1] > d) { kd[i] = kd[i - 1]; kn[i] = kn[i - 1]; }
+          else if (kd[i] > d) { kd[i] = d; kn[i] = n; }
+        }
+        if (kd[0] > d) { kd[0] = d; kn[0] = n; }
+      }
+    }
+  }
+  // myROI.calcROI variants (myTextureHandler.java:515-690) over the ascending distinct distances
+  double dist = 0;
+  int i = 0;
+  double mod = -1;
+#pragma unroll
+  for (int q = 0; q < KD; ++q) {
+    if (kd[q] == INFINITY) break;
+    const double k = kd[q];
+    switch (m.roiFunc) {
+      case 0: dist += k; i++; break;                        // nearestROI
+      case 2: dist += 1.0 / (mod * k); i++; break;          // altInvLinROI
+      case 3: dist += (mod * pow(k, (double)(++i))); break;  // altExpROI
+      case 4: dist += (mod * log(1 + k)); i++; break;       // altLogROI
+      case 5: dist += pow(k, (double)(++i)); break;          // linExpROI
+      case 6: dist += log(1 + k); i++; break;               // linLogROI
+      case 7: dist += pow(k, (double)-(++i)); break;         // invExpROI
+      case 8: dist += 1.0 / log(1 + k); i++; break;         // invLogROI
+      default: dist += (mod * k); i++; break;               // altLinROI (1 and unknown)
+    }
+    if (i >= m.numPtsDist) break;
+    mod *= -1;
+  }
+  if (m.roiFunc != 6) {  // fixDist (linLogROI returns its sum unfixed)
+    if (dist < 0) dist *= -1;
+    if (dist > 1.0) dist = 1.0 / dist;
+  }
+  dist = (dist < 0 ? 0 : dist > 1 ? 1 : dist);
+  int brick = 0;
+  if (!(dist < m.mortar)) {
+    const int nb = kn[0];
+    const int dx = (nb / 9 == 2) ? -1 : nb / 9, dy = ((nb / 3) % 3 == 2) ? -1 : (nb / 3) % 3, dz = (nb % 3 == 2) ? -1 : nb % 3;
+    rnd.seed(hash_ints(ix + dx, iy + dy, iz + dz));
+    const double res = rnd.next_double();
+    brick = 2 * (1 + fastfloor(((m.ncolors / 2) - 1) * res));
+  }
+  return clr_ara(m, .65, hv, brick, brick + 1);
 }
 
 // getDiffTxtrColor of the shader's texture handler (myTextureHandler.java)
@@ -484,6 +582,11 @@ DEVI V diff_color(const SceneD& S, const MatD& m, const HitRec& h, const Key& k,
     if (m.tex == 1) {  // myImageTexture :105-117
       V c = (m.texTop >= 0) ? image_color<CNT>(S, h, k, S.tex[m.texTop], ct) : ld3(m.diffuse);
       return mk(c.x * diffConst, c.y * diffConst, c.z * diffConst);
+    }
+    if (m.tex == 5) {
+      V out = cellular_color(m, h);
+      if (fabs(diffConst - 1.0) > EPS) out = mk(out.x * diffConst, out.y * diffConst, out.z * diffConst);
+      return out;
     }
     if (m.tex == 2 || m.tex == 3 || m.tex == 4 || m.tex == 6) {
       V hv = m.useFwdTrans ? h.fwd : h.hitLoc;

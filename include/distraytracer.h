@@ -73,7 +73,9 @@ typedef struct rt_prim_desc {
 } rt_prim_desc;
 
 /* myScene.txtrType (myScene.java:117, getCurTexture :531-542) */
-enum rt_texture_kind { RT_TEX_NONE = 0, RT_TEX_IMAGE = 1, RT_TEX_NOISE = 2, RT_TEX_WOOD = 3, RT_TEX_MARBLE = 4, RT_TEX_WOOD2 = 6 };
+enum rt_texture_kind { RT_TEX_NONE = 0, RT_TEX_IMAGE = 1, RT_TEX_NOISE = 2, RT_TEX_WOOD = 3, RT_TEX_MARBLE = 4,
+                       RT_TEX_STONE = 5, RT_TEX_WOOD2 = 6 };
+#define RT_MAX_NOISE_COLORS 16
 
 typedef struct rt_material_desc { /* myObjShader.setCurrColors (myObjShader.java:51-75) */
   int32_t simple;       /* 1 = mySimpleReflObjShdr (`shiny` with ktrans/index) */
@@ -84,7 +86,11 @@ typedef struct rt_material_desc { /* myObjShader.setCurrColors (myObjShader.java
   double diffuse[3], ambient[3], specular[3]; /* already clamped <= 1 (myColor) */
   double phong_exp, k_refl, k_refl_clr[3], k_trans, perm, perm_clr[3];
   double noise_scale, turb_mult, color_scale, color_mult, period_mult[3];
-  double colors[2][3];  /* the two noise colours the Perlin textures interpolate (getClrAra idx 0, 1) */
+  double colors[RT_MAX_NOISE_COLORS][3]; /* noise colours (noise_color list or the texture's defaults) */
+  int32_t num_colors;
+  /* RT_TEX_STONE (myCellularTexture): 0 Manhattan / 1 Euclid, ROI function 0..8, points per ROI */
+  int32_t dist_func, roi_func, num_pts_dist;
+  double avg_per_cell, mortar_thresh;
 } rt_material_desc;
 
 enum rt_light_type { RT_LIGHT_POINT = 0, RT_LIGHT_SPOT = 1, RT_LIGHT_DISK = 2 };

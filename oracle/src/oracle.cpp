@@ -15,6 +15,7 @@
 // fixtures it generates (tests/golden/). ThreadLocalRandom is replaced by the
 // keyed counter RNG of jmath.h (the reference is not seedable).
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -231,7 +232,7 @@ struct BBox : GeomBase {
 
 // ---------------------------------------------------------------------------
 // shaders (myObjShader.java)
-enum TexKind { TX_NONE = 0, TX_IMAGE = 1, TX_NOISE = 2, TX_WOOD = 3, TX_MARBLE = 4, TX_WOOD2 = 6 };
+enum TexKind { TX_NONE = 0, TX_IMAGE = 1, TX_NOISE = 2, TX_WOOD = 3, TX_MARBLE = 4, TX_STONE = 5, TX_WOOD2 = 6 };
 struct Shader {
   bool simple = false;  // mySimpleReflObjShdr
   Color diffuse, ambient, specular, curPermClr, KReflClr;
@@ -249,6 +250,10 @@ struct Shader {
   V3 periodMult{10, 10, 10};
   bool rndColors = false, useFwdTrans = false;
   std::vector<Color> colors;
+  // myCellularTexture (myTextureHandler.java:380-498)
+  int numPtsDist = 2, distFunc = 1, roiFunc = 1;
+  double mortarThresh = 0.05;
+  std::map<double, int> pdfs;  // cumulative Poisson probability -> # points (ConcurrentSkipListMap, put replaces)
 };
 
 // ---------------------------------------------------------------------------
@@ -1003,7 +1008,7 @@ static void image_color(Hit& hit, const Texture& tex, double out[3], uint64_t* s
   Color c0 = lerp(c00, fu, c01), c1 = lerp(c10, fu, c11), c = lerp(c0, fv, c1);
   out[0] = c.r; out[1] = c.g; out[2] = c.b;
 }
-static void clr_ara(const Shader* sh, double distVal, const V3& raw, double res[3]) {  // getClrAra :277-294
+static void clr_ara(const Shader* sh, double distVal, const V3& raw, double res[3], int i0 = 0, int i1 = 1) {  // getClrAra :277-294
   V3 pt(raw.x * sh->colorScale, raw.y * sh->colorScale, raw.z * sh->colorScale);
   double mult = sh->colorMult;
   double rm[3] = {1.0, 1.0, 1.0};
@@ -1012,7 +1017,7 @@ static void clr_ara(const Shader* sh, double distVal, const V3& raw, double res[
     rm[1] = 1.0 + (mult * noise3((float)pt.y, (float)pt.x, (float)pt.z));
     rm[2] = 1.0 + (mult * noise3((float)pt.z, (float)pt.y, (float)pt.x));
   }
-  const Color &c0 = sh->colors[0], &c1 = sh->colors[1];
+  const Color &c0 = sh->colors.at(i0), &c1 = sh->colors.at(i1);
   res[0] = jmax(0, jmin(1.0, (c0.r) + rm[0] * distVal * ((c1.r) - (c0.r))));
   res[1] = jmax(0, jmin(1.0, (c0.g) + rm[1] * distVal * ((c1.g) - (c0.g))));
   res[2] = jmax(0, jmin(1.0, (c0.b) + rm[2] * distVal * ((c1.b) - (c0.b))));
@@ -1048,11 +1053,93 @@ static bool named_color(std::string n, Color& c) {
   return true;
 }
 
+// java.util.Random (JDK 8): 48-bit LCG, setSeed scrambling, nextDouble from 26 + 27 bits
+struct JRandom {
+  uint64_t seed = 0;
+  void set_seed(int64_t s) { seed = ((uint64_t)s ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1); }
+  int32_t next(int bits) {
+    seed = (seed * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+    return (int32_t)(int64_t)(seed >> (48 - bits));
+  }
+  double next_double() { return (double)(((int64_t)next(26) << 27) + next(27)) * 0x1.0p-53; }
+};
+static int fastfloor(double x) { return x > 0 ? jd2i(x) : jd2i(x) - 1; }  // DistRayTracer.java:307
+// myROI.calcROI variants (myTextureHandler.java:515-690) over the ascending distinct distances
+static double roi(int fn, int numPts, const std::vector<double>& keys) {
+  auto fix = [](double d) { if (d < 0) d *= -1; if (d > 1.0) d = 1.0 / d; return d; };
+  double dist = 0;
+  int i = 0, mod = -1;
+  for (double k : keys) {
+    switch (fn) {
+      case 0: dist += k; i++; break;                                 // nearestROI
+      case 2: dist += 1.0 / (mod * k); i++; break;                   // altInvLinROI
+      case 3: dist += (mod * std::pow(k, ++i)); break;               // altExpROI
+      case 4: dist += (mod * std::log(1 + k)); i++; break;           // altLogROI
+      case 5: dist += std::pow(k, ++i); break;                       // linExpROI
+      case 6: dist += std::log(1 + k); i++; break;                   // linLogROI
+      case 7: dist += std::pow(k, -(++i)); break;                    // invExpROI
+      case 8: dist += 1.0 / std::log(1 + k); i++; break;             // invLogROI
+      default: dist += (mod * k); i++; break;                        // altLinROI (1 and unknown)
+    }
+    if (i >= numPts) break;
+    mod *= -1;
+  }
+  return fn == 6 ? dist : fix(dist);  // linLogROI returns its sum unfixed
+}
+static const int NGHBR[27][3] = {  // DistRayTracer.nghbrHdCells (:21-25)
+    {0, 0, 0},  {0, 0, 1},  {0, 0, -1},  {0, 1, 0},  {0, 1, 1},  {0, 1, -1},  {0, -1, 0},  {0, -1, 1},  {0, -1, -1},
+    {1, 0, 0},  {1, 0, 1},  {1, 0, -1},  {1, 1, 0},  {1, 1, 1},  {1, 1, -1},  {1, -1, 0},  {1, -1, 1},  {1, -1, -1},
+    {-1, 0, 0}, {-1, 0, 1}, {-1, 0, -1}, {-1, 1, 0}, {-1, 1, 1}, {-1, 1, -1}, {-1, -1, 0}, {-1, -1, 1}, {-1, -1, -1}};
+static int32_t hash_ints(int32_t x, int32_t y, int32_t z) {  // hashInts, Java int arithmetic (wraps)
+  return (int32_t)((uint32_t)x * 1572869u + (uint32_t)y * 6291469u + (uint32_t)z);
+}
+// myCellularTexture.getDiffTxtrColor (myTextureHandler.java:433-480)
+static void cellular_color(const Shader* sh, Hit& hit, double out[3]) {
+  V3 hv = sh->useFwdTrans ? hit.fwdTransHitLoc : hit.hitLoc;
+  hv = V3(hv.x * sh->scale, hv.y * sh->scale, hv.z * sh->scale);
+  const int idx[3] = {fastfloor(hv.x), fastfloor(hv.y), fastfloor(hv.z)};
+  std::map<double, std::array<int32_t, 3>> distToPts;  // put replaces the cell of an equal distance
+  JRandom rnd;
+  for (int n = 0; n < 27; ++n) {
+    std::array<int32_t, 3> cell = {idx[0] + NGHBR[n][0], idx[1] + NGHBR[n][1], idx[2] + NGHBR[n][2]};
+    rnd.set_seed(hash_ints(cell[0], cell[1], cell[2]));
+    double prob = rnd.next_double();
+    auto it = sh->pdfs.lower_bound(prob);  // lowerKey(prob): greatest key < prob, else firstKey
+    int numPoints = (it == sh->pdfs.begin()) ? sh->pdfs.begin()->second : std::prev(it)->second;
+    for (int j = 0; j < numPoints; ++j) {
+      double px = cell[0] + rnd.next_double(), py = cell[1] + rnd.next_double(), pz = cell[2] + rnd.next_double();
+      double d = (sh->distFunc == 0)
+                     ? std::fabs(hv.x - px) + std::fabs(hv.y - py) + std::fabs(hv.z - pz)  // _L1Dist
+                     : std::sqrt(((hv.x - px) * (hv.x - px)) + ((hv.y - py) * (hv.y - py)) + ((hv.z - pz) * (hv.z - pz)));
+      distToPts[d] = cell;
+    }
+  }
+  std::vector<double> keys;
+  for (auto& e : distToPts) keys.push_back(e.first);
+  double dist = roi(sh->roiFunc, sh->numPtsDist, keys);
+  dist = (dist < 0 ? 0 : dist > 1 ? 1 : dist);
+  int brick = 2;
+  if (dist < sh->mortarThresh) {
+    brick = 0;
+  } else {
+    const std::array<int32_t, 3>& c0 = distToPts.begin()->second;
+    rnd.set_seed(hash_ints(c0[0], c0[1], c0[2]));
+    double res = rnd.next_double();
+    brick = 2 * (1 + (fastfloor((((int)sh->colors.size() / 2) - 1) * res)));
+  }
+  clr_ara(sh, .65, hv, out, brick, brick + 1);
+}
+
 static void diff_txtr_color(Shader* sh, Hit& hit, double diffConst, double out[3], uint64_t* st) {
   if (sh->tex == TX_IMAGE) {  // myImageTexture.getDiffTxtrColor :105-117
     if (sh->txTop && sh->texTop) image_color(hit, *sh->texTop, out, st);
     else { out[0] = sh->diffuse.r; out[1] = sh->diffuse.g; out[2] = sh->diffuse.b; }
     out[0] *= diffConst; out[1] *= diffConst; out[2] *= diffConst;
+    return;
+  }
+  if (sh->tex == TX_STONE) {
+    cellular_color(sh, hit, out);
+    if (std::fabs(diffConst - 1.0) > EPS) { out[0] *= diffConst; out[1] *= diffConst; out[2] *= diffConst; }
     return;
   }
   if (sh->tex == TX_NOISE || sh->tex == TX_MARBLE || sh->tex == TX_WOOD || sh->tex == TX_WOOD2) {
@@ -1483,6 +1570,8 @@ struct Loader {
   V3 pdMult{10, 10, 10};
   bool rndColors = false, useFwdTrans = false, useCustClrs = false;
   std::vector<Color> noiseColors{Color(.7, .7, .7), Color(.2, .2, .2)};
+  int numPtsDist = 2, distFunc = 1, roiFunc = 1;
+  double avgNumPerCell = 1.0, mortarThresh = 0.05;
   bool inTmpList = false;
   std::vector<GeomBase*> tmpList;
   int curNumRaysPerPxl = 0;
@@ -1519,7 +1608,7 @@ struct Loader {
     sh->isCausticPhtn = s->isCausticPhtn;
     sh->diffConst = 1 - rfrIdx;
     sh->phongExp = phong;
-    sh->tex = (txtrType == 1 || txtrType == 2 || txtrType == 3 || txtrType == 4 || txtrType == 6) ? txtrType : TX_NONE;
+    sh->tex = (txtrType >= 1 && txtrType <= 6) ? txtrType : TX_NONE;
     if (txtrType == 1) {
       sh->txTop = txTop;
       if (txTop) {
@@ -1528,7 +1617,16 @@ struct Loader {
         else sh->texTop = &it->second;
       }
     }
-    if (txtrType == 2 || txtrType == 3 || txtrType == 4 || txtrType == 6) {
+    if (txtrType == 5) {  // myCellularTexture ctor (myTextureHandler.java:390-425)
+      sh->numPtsDist = numPtsDist; sh->distFunc = distFunc; sh->roiFunc = roiFunc; sh->mortarThresh = mortarThresh;
+      double lastDist = 1.0 / std::pow(M_E, avgNumPerCell), cumProb = lastDist;
+      for (int i = 1; i < 15; ++i) {
+        lastDist *= (avgNumPerCell / (1.0 * i));
+        cumProb += lastDist;
+        sh->pdfs[cumProb] = i;
+      }
+    }
+    if (txtrType == 2 || txtrType == 3 || txtrType == 4 || txtrType == 5 || txtrType == 6) {
       while (noiseColors.size() < 2) noiseColors.push_back(Color(1, 1, 1));  // (Java would throw at render)
       sh->scale = noiseScale; sh->numOctaves = numOctaves; sh->turbMult = turbMult; sh->periodMult = pdMult;
       sh->colorScale = colorScale; sh->colorMult = colorMult; sh->rndColors = rndColors; sh->useFwdTrans = useFwdTrans;
@@ -1546,6 +1644,27 @@ struct Loader {
     noiseScale = 1.0; turbMult = 1.0; colorScale = 5.0; colorMult = .1;
     pdMult = V3(1.0, 1.0, 1.0);
     noiseColors = {Color(0.05, 0.05, 0.05), Color(1.0, 1.0, 1.0)};
+    numPtsDist = 2; distFunc = 1; roiFunc = 1; avgNumPerCell = 1.0; mortarThresh = 0.05;
+  }
+  bool read_worley(const std::vector<std::string>& v) {  // readProcTxtrWorleyVals (myScene.java:675-708)
+    try {
+      size_t k = 1;
+      noiseScale = std::stod(v.at(k++));
+      distFunc = std::stoi(v.at(k++));
+      roiFunc = std::stoi(v.at(k++));
+      numPtsDist = std::stoi(v.at(k++));
+      avgNumPerCell = std::stod(v.at(k++));
+      mortarThresh = std::stod(v.at(k++));
+      useFwdTrans = (std::stod(v.at(k++)) == 1.0);
+      if (v.size() >= k + 2) {
+        colorScale = std::stod(v.at(k)); colorMult = std::stod(v.at(k + 1)); rndColors = true;
+      } else {
+        rndColors = false; colorScale = 25.0; colorMult = .1;
+      }
+      return false;
+    } catch (...) {
+      return true;
+    }
   }
   bool read_perlin(const std::vector<std::string>& v) {  // readProcTxtrPerlinVals (myScene.java:642-672)
     try {
@@ -1766,9 +1885,19 @@ struct Loader {
             col = Color(num(t, 1), num(t, 2), num(t, 3));
           }
           noiseColors.push_back(col);
-        } else if (c == "stone") {
-          err = "unsupported texture command (cellular texture, out of scope): " + c;
-          return false;
+        } else if (c == "stone") {  // setTexture (myScene.java:756-771)
+          reset_dflt_txtr();
+          txtrType = 5;
+          bool dflt = read_worley(t);
+          if (!useCustClrs)
+            noiseColors = {Color(0.2, 0.2, 0.2), Color(0.7, 0.7, 0.7), Color(0.6, 0.18, 0.22), Color(0.8, 0.26, 0.33),
+                           Color(0.6, 0.32, 0.16), Color(0.8, 0.45, 0.25), Color(0.3, 0.01, 0.07), Color(0.6, 0.02, 0.13),
+                           Color(0.4, 0.1, 0.17), Color(0.6, 0.3, 0.13)};  // clr_mortar1/2, clr_brick1_1 .. clr_brick4_2
+          if (dflt) {
+            numOctaves = 8; numPtsDist = 2; distFunc = 1; roiFunc = 1; rndColors = true; useFwdTrans = false;
+            noiseScale = 4.0; turbMult = 1.0; colorScale = 12.0; colorMult = .2; avgNumPerCell = 1.0; mortarThresh = 0.05;
+            pdMult = V3(10.0, 10.0, 10.0);
+          }
         } else if (c == "begin") {
           vertType = t.size() > 1 ? t[1] : "triangle";
           vc = 0;

@@ -64,7 +64,8 @@ def test_host_builder_matches_oracle_topology(cfg):
 
 @pytest.mark.parametrize("cli", ["p2_t03.cli", "p2_t05.cli", "p2_t07.cli", "c2clear.cli", "t05.cli", "p3_t05.cli",
                                  "earth.cli", "cylinder1.cli", "old_t07.cli", "old_t10.cli", "planets3Ortho.cli",
-                                 "p3_t09.cli", "p4_t05.cli", "p4_t06_2.cli"])
+                                 "p3_t09.cli", "p4_t05.cli", "p4_t06_2.cli"] +
+                                [f"p4_st0{i}.cli" for i in range(1, 10)])
 def test_host_builder_feature_scenes(cli):
     scenes.ensure_bun69k()
     tex = scenes.prepare(cli)

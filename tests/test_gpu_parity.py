@@ -81,6 +81,16 @@ def test_feature_scenes_parity(cli, spp):
     assert c["mismatch_frac"] < 2e-3, c
 
 
+@pytest.mark.parametrize("cli", [f"p4_st0{i}.cli" for i in range(1, 10)])
+def test_stone_parity(cli):
+    """cellular `stone` texture (myCellularTexture, myTextureHandler.java:380-498): st01-st07 walk
+    the ROI functions 2..8 with Euclid distance, st08 nearestROI with Manhattan distance,
+    st09 altExpROI; all read worleyClrs.cli (10 noise colours)."""
+    g, o, (rg, ag), (ro, ao) = both(cli, 96, 96, 1)
+    c = compare(rg, ag, ro, ao)
+    assert c["mismatch_frac"] < 2e-3, c
+
+
 def test_c3_full_size_properties():
     """BASELINE C3 size (1024^2, 16 spp): deterministic, band-decomposable, and
     matching the oracle on a row subsample."""
