@@ -57,7 +57,7 @@ static bool named_color(std::string n, Clr& c) {
 }
 
 struct CliLoader {
-  std::string dir;
+  std::string dir, saveName;
   std::map<std::string, int> texIndex;
   std::vector<Mat> stack{Mat::ident()};
   // material state
@@ -236,6 +236,7 @@ struct CliLoader {
         } else if (c == "lens") {
           d.dof = 1; d.lens_radius = num(t, 1); d.lens_focal = num(t, 2);
         } else if (c == "write") {
+          if (saveName.empty()) saveName = t.at(1);  // scene.saveName (:87)
           break;  // the reference renders here (:86-93)
         } else if (c == "read") {
           if (!read(t.at(1), false)) return false;
@@ -510,7 +511,31 @@ extern "C" int rt_scene_load_cli(const char* scene_dir, const char* cli_file, in
   CliLoader L;
   int rc = load_desc(scene_dir, cli_file, num_textures, texture_names, textures, L);
   if (rc) return rc;
-  return rt_scene_create(&L.d, device, out);
+  rc = rt_scene_create(&L.d, device, out);
+  if (rc == RT_OK) (*out)->saveName = L.saveName.empty() ? std::string(cli_file) : L.saveName;
+  return rc;
+}
+
+static int put_name(const std::string& n, char* buf, int cap) {
+  if (buf && cap > (int)n.size()) std::memcpy(buf, n.c_str(), n.size() + 1);
+  return (int)n.size();
+}
+
+// myScene.saveFile (myScene.java:1185-1196): saveName.split("\\.(?=[^\\.]+$)")[0] + ".png" --
+// cut at the last '.' when at least one non-'.' character follows it (flipNormal's
+// "_normFlipped" suffix is a UI action, not part of the render path).
+extern "C" int rt_png_name(const char* save_name, char* buf, int cap) {
+  if (!save_name) return set_error(RT_E_INVALID, "rt_png_name: null name");
+  std::string n = save_name;
+  size_t dot = n.rfind('.');
+  if (dot != std::string::npos && dot + 1 < n.size()) n.resize(dot);
+  return put_name(n + ".png", buf, cap);
+}
+
+extern "C" int rt_scene_save_name(const rt_scene* s, char* buf, int cap) {
+  if (!s) return set_error(RT_E_INVALID, "rt_scene_save_name: null scene");
+  if (s->saveName.empty()) return set_error(RT_E_INVALID, "rt_scene_save_name: scene not loaded from a .cli");
+  return rt_png_name(s->saveName.c_str(), buf, cap);
 }
 
 // Host-only: parse + build the flattened scene without touching a device, report the

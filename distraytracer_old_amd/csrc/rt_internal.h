@@ -56,6 +56,7 @@ void build_photon_tree(HostScene& hs, const std::vector<double>& pos, const std:
 
 struct rt_scene {
   rt::HostScene hs;
+  std::string saveName;  // `write` argument (or the .cli name) when loaded by rt_scene_load_cli
   int device = 0;
   rt::SceneD dev{};
   std::vector<void*> allocs;

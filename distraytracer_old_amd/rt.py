@@ -39,7 +39,8 @@ class RenderParams(ctypes.Structure):
 EXPORTS = ["rt_abi_version", "rt_last_error", "rt_device_count", "rt_scene_create", "rt_scene_load_cli",
            "rt_scene_inspect_cli",
            "rt_scene_info", "rt_scene_destroy", "rt_photons_build", "rt_render", "rt_render_device",
-           "rt_render_count", "rt_time_render", "rt_scene_photons", "rt_photons_shoot", "rt_photons_set"]
+           "rt_render_count", "rt_time_render", "rt_scene_photons", "rt_photons_shoot", "rt_photons_set",
+           "rt_png_name", "rt_scene_save_name"]
 
 _lib = None
 
@@ -80,8 +81,24 @@ def lib():
                                        ctypes.c_void_p, ctypes.c_void_p]
         L.rt_time_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_double)]
+        L.rt_png_name.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+        L.rt_scene_save_name.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
         _lib = L
     return _lib
+
+
+def _name_call(fn, *args) -> str:
+    n = fn(*args, None, 0)
+    if n < 0:
+        raise RTError(f"{fn.__name__} failed ({n}): {lib().rt_last_error().decode()}")
+    buf = ctypes.create_string_buffer(n + 1)
+    fn(*args, buf, n + 1)
+    return buf.value.decode()
+
+
+def png_name(save_name: str) -> str:
+    """myScene.saveFile's image name for a `write` argument (myScene.java:1185-1196)."""
+    return _name_call(lib().rt_png_name, save_name.encode())
 
 
 def _check(rc: int, what: str):
@@ -151,6 +168,10 @@ class Scene:
         v = np.zeros(len(INFO_NAMES), dtype=np.int64)
         _check(lib().rt_scene_info(self._h, v.ctypes.data, len(INFO_NAMES)), "rt_scene_info")
         return dict(zip(INFO_NAMES, v.tolist()))
+
+    def save_name(self) -> str:
+        """PNG name of the scene's `write` command (rt_scene_save_name)."""
+        return _name_call(lib().rt_scene_save_name, self._h)
 
     def build_photons(self, seed: int):
         _check(lib().rt_photons_build(self._h, seed), "rt_photons_build")

@@ -185,6 +185,13 @@ int rt_scene_inspect_cli(const char* scene_dir, const char* cli_file, int num_te
    device bytes, triangles, photons (stored), materials, photon mode (0 none / 1 diffuse / 2 caustic),
    photons emitted per light */
 int rt_scene_info(const rt_scene* scene, int64_t* info, int n);
+/* PNG name myScene.saveFile gives the image (myScene.java:1185-1196): the `write` argument
+   (myRTFileReader.java:86-88; the .cli file name when the file has none) with its last
+   extension removed, plus ".png". rt_png_name applies the rule to any name; rt_scene_save_name
+   to the name recorded by rt_scene_load_cli (RT_E_INVALID for a scene built from a desc).
+   Both return the name's length, writing it NUL-terminated when it fits in cap. */
+int rt_png_name(const char* save_name, char* buf, int cap);
+int rt_scene_save_name(const rt_scene* scene, char* buf, int cap);
 void rt_scene_destroy(rt_scene* scene);
 
 /* photon-map pre-pass (myScene.initRender :1096-1099); idempotent per scene */

@@ -19,6 +19,29 @@ def test_driver_builds_and_fails_loudly_without_gpu():
     assert r.returncode == 2 and "usage" in r.stderr
 
 
+@pytest.mark.parametrize("name,png", [("t01.png", "t01.png"), ("t01", "t01.png"), ("a.b.png", "a.b.png"),
+                                      ("dir.x/t01", "dir.png"), ("abc.", "abc..png"), ("x.y.", "x.y..png"),
+                                      ("scenes/t03.cli", "scenes/t03.png"), (".png", ".png")])
+def test_png_name_rule(name, png):
+    """myScene.saveFile: split("\\.(?=[^\\.]+$)")[0] + ".png" (myScene.java:1188-1192)."""
+    from distraytracer_old_amd import rt
+    assert rt.png_name(name) == png
+
+
+@pytest.mark.gpu
+def test_driver_default_output_name(tmp_path):
+    """no -o: pics.<date>/<write name>.png (t01.cli ends with `write t01.png`); -nodir: cwd."""
+    exe = build()
+    r = subprocess.run([str(exe), str(REPO / "scenes"), "t01.cli", "-w", "32", "-h", "32"], cwd=tmp_path,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    pics = [p for p in tmp_path.iterdir() if p.name.startswith("pics.")]
+    assert len(pics) == 1 and (pics[0] / "t01.png").exists(), list(tmp_path.iterdir())
+    r = subprocess.run([str(exe), str(REPO / "scenes"), "t01.cli", "-w", "32", "-h", "32", "-nodir"], cwd=tmp_path,
+                       capture_output=True, text=True)
+    assert r.returncode == 0 and (tmp_path / "t01.png").exists(), r.stderr
+
+
 @pytest.mark.gpu
 def test_driver_t01_png_kat(tmp_path):
     from PIL import Image

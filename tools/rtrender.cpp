@@ -3,14 +3,23 @@
 // calls myScene.draw() and saves rndrdImg as PNG (myScene.java:1185-1196).
 //
 //   rtrender <scene_dir> <file.cli> [-w W] [-h H] [-spp N] [-seed S] [-device D] [-o out.png]
-//            [-rgb out.f32] [-tex name=path.ppm]... [-time ITERS]
+//            [-rgb out.f32] [-tex name=path.ppm]... [-time ITERS] [-nodir]
+//
+// Without -o the image goes where myScene.saveFile puts it (myScene.java:1185-1196): the
+// `write` name (rt_scene_save_name) inside the folder "pics.<yyyy.MM.dd.hh.mm>" the scene
+// creates (myScene.java:170, getDateTimeString :1329-1340; saveImgInDir defaults on :182),
+// or in the current directory with -nodir. '/' separates the folder (the reference
+// concatenates a Windows "\\").
 //
 // Textures are binary PPM (P6, 8-bit) files, one per texture name the .cli references
 // (tools/textures_to_ppm.py converts the scene textures with the same decoder the tests use).
 // Build: tools/build_rtrender.sh (links libdistraytracer.so and zlib).
 #include <zlib.h>
 
+#include <sys/stat.h>
+
 #include <cstdio>
+#include <ctime>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -77,10 +86,11 @@ static bool write_png(const std::string& path, int w, int h, const int32_t* argb
 int main(int argc, char** argv) {
   if (argc < 3) {
     std::fprintf(stderr, "usage: %s <scene_dir> <file.cli> [-w W] [-h H] [-spp N] [-seed S] [-device D] "
-                         "[-o out.png] [-rgb out.f32] [-tex name=path.ppm]... [-time ITERS]\n", argv[0]);
+                         "[-o out.png] [-rgb out.f32] [-tex name=path.ppm]... [-time ITERS] [-nodir]\n", argv[0]);
     return 2;
   }
-  std::string dir = argv[1], cli = argv[2], out = "out.png", rgbOut;
+  std::string dir = argv[1], cli = argv[2], out, rgbOut;
+  bool inDir = true;
   int W = 300, H = 300, spp = 0, device = 0, timeIters = 0;  // DistRayTracer.java:15-16 default size
   uint64_t seed = 0x5EED0001ull;
   std::vector<std::string> texNames, texPaths;
@@ -98,6 +108,7 @@ int main(int argc, char** argv) {
     else if (a == "-o") out = next();
     else if (a == "-rgb") rgbOut = next();
     else if (a == "-time") timeIters = std::atoi(next().c_str());
+    else if (a == "-nodir") inDir = false;
     else if (a == "-tex") {
       std::string t = next();
       size_t eq = t.find('=');
@@ -118,6 +129,21 @@ int main(int argc, char** argv) {
   rt_scene* s = nullptr;
   int rc = rt_scene_load_cli(dir.c_str(), cli.c_str(), (int)tex.size(), names.data(), tex.data(), device, &s);
   if (rc) { std::fprintf(stderr, "rt_scene_load_cli: %d %s\n", rc, rt_last_error()); return 1; }
+  if (out.empty()) {
+    char name[4096];
+    int n = rt_scene_save_name(s, name, (int)sizeof(name));
+    if (n < 0 || n >= (int)sizeof(name)) { std::fprintf(stderr, "rt_scene_save_name: %s\n", rt_last_error()); return 1; }
+    out = name;
+    if (inDir) {
+      std::time_t now = std::time(nullptr);
+      std::tm tm = *std::localtime(&now);
+      char folder[64];  // Calendar.HOUR: 12-hour clock, 0-11
+      std::snprintf(folder, sizeof(folder), "pics.%d.%02d.%02d.%02d.%02d", tm.tm_year + 1900, tm.tm_mon + 1, tm.tm_mday,
+                    tm.tm_hour % 12, tm.tm_min);
+      mkdir(folder, 0755);
+      out = std::string(folder) + "/" + out;
+    }
+  }
   rt_render_params p;
   std::memset(&p, 0, sizeof(p));
   p.width = W; p.height = H; p.spp = spp; p.row0 = 0; p.row1 = H; p.row_step = 1; p.seed = seed;
