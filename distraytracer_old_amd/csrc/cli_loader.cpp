@@ -5,8 +5,7 @@
 // stack). It emits the flattened rt_scene_desc that a JNI myScene subclass
 // would hand over, then calls rt_scene_create().
 //
-// Commands outside the hot-path scope (instances, sierpinski) are rejected
-// with RT_E_PARSE.
+// Commands outside the hot-path scope are rejected with RT_E_PARSE.
 #include <cctype>
 #include <fstream>
 #include <map>
@@ -80,6 +79,9 @@ struct CliLoader {
   std::vector<rt_light_desc> lights;
   std::vector<rt_accel_desc> accels;
   std::vector<int32_t> members, top;
+  std::vector<rt_instance_desc> insts;
+  std::map<std::string, int32_t> named;  // namedObjs (myScene.java:378-387): prim index or ~accel
+  bool lastWasLight = false;             // allObjsToFind's last entry is a light
   bool inList = false;
   std::vector<int32_t> tmp;
   rt_scene_desc d{};
@@ -134,6 +136,101 @@ struct CliLoader {
     prims.push_back(p);
     if (inList) tmp.push_back(idx);
     else top.push_back(idx);
+    lastWasLight = false;
+  }
+  // gtTranslate / gtScale / gtRotate (myScene.java:1256-1318)
+  void translate(double x, double y, double z) {
+    Mat T = Mat::ident();
+    T.m[3] = x; T.m[7] = y; T.m[11] = z;
+    stack.back() = mul(stack.back(), T);
+  }
+  void scale(double x, double y, double z) {
+    Mat S = Mat::ident();
+    S.m[0] = x; S.m[5] = y; S.m[10] = z;
+    stack.back() = mul(stack.back(), S);
+  }
+  void rotate(double ang, double ax, double ay, double az) {
+    double ar = (double)(ang * M_PI) / 180.0;
+    D3 av = normalized(d3(ax, ay, az));
+    D3 nv = (ax == 0) ? d3(1, 0, 0) : d3(0, 1, 0);
+    D3 bv = normalized(cross(av, nv));
+    D3 cv = normalized(cross(av, bv));
+    Mat R1 = Mat::ident(), R2 = Mat::ident();
+    R1.m[0] = av.x; R1.m[1] = av.y; R1.m[2] = av.z;
+    R1.m[4] = bv.x; R1.m[5] = bv.y; R1.m[6] = bv.z;
+    R1.m[8] = cv.x; R1.m[9] = cv.y; R1.m[10] = cv.z;
+    R2.m[5] = std::cos(ar); R2.m[6] = -std::sin(ar); R2.m[9] = std::sin(ar); R2.m[10] = std::cos(ar);
+    stack.back() = mul(stack.back(), mul(transpose(R1), mul(R2, R1)));
+  }
+  void push() { stack.push_back(stack.back()); }  // gtPushMatrix :1241-1246
+  void pop() { if (stack.size() > 1) stack.pop_back(); }
+  // addInstance (myScene.java:389-395) + myInstance ctor (mySceneObject.java:98-110)
+  bool add_instance(const std::string& name, bool addShdr) {
+    auto it = named.find(name);
+    if (it == named.end()) { err = "unknown named object: " + name; return false; }
+    rt_instance_desc in;
+    std::memset(&in, 0, sizeof(in));
+    in.base = it->second;
+    Mat bg;
+    std::memcpy(bg.m, in.base >= 0 ? prims[in.base].ctm : accels[~in.base].ctm, sizeof(bg.m));
+    Mat g = mul(bg, stack.back());  // buildCTMara(scene, obj.CTMara[glbl]) = obj glbl x stack top
+    std::memcpy(in.ctm, g.m, sizeof(in.ctm));
+    D3 o = xform(stack.back(), d3(0, 0, 0), 1);
+    in.origin[0] = o.x; in.origin[1] = o.y; in.origin[2] = o.z;
+    in.material = addShdr ? material() : -1;  // useInstShader: getCurShader()
+    int32_t ref = RT_INSTANCE_REF((int32_t)insts.size());
+    insts.push_back(in);
+    if (inList) tmp.push_back(ref);
+    else top.push_back(ref);
+    lastWasLight = false;
+    return true;
+  }
+  // setSierpShdr (myScene.java:328-337), float arithmetic as in the reference
+  void sierp_shader(int level, int maxLevel) {
+    float bVal = 1.0f - std::min(1.0f, (1.5f * level / maxLevel)), rVal = 1.0f - bVal,
+          tmpv = std::min((1.2f * (level - (maxLevel / 2))) / (1.0f * maxLevel), 1.0f), gVal = (tmpv * tmpv);
+    txTop = false;
+    set_surface(clr(std::min(1.0f, rVal + .5f), std::min(1.0f, gVal + .5f), std::min(1.0f, bVal + .5f)), clr(0, 0, 0),
+                clr(0, 0, 0), 0, 0);
+  }
+  void sierp_shift(float newTrans) { rotate(120, 1, 0, 0); translate(0, newTrans, 0); rotate(-120, 1, 0, 0); }
+  // buildSierpSubTri (myScene.java:339-369): one instance per call, then four scaled sub-tetrahedra
+  bool sierp_sub(float dim, float scVal, const std::string& name, int level, int maxLevel, bool addShader) {
+    if (level >= maxLevel) return true;
+    float newDim = scVal * dim;
+    push();
+    translate(0, .1f * dim, 0);
+    rotate(70, 0, 1, 0);
+    if (addShader) sierp_shader(level, maxLevel);
+    if (!add_instance(name, addShader)) return false;
+    pop();
+    const float sqrt66 = (float)std::sqrt(6.0f) / 6.0f;  // DistRayTracer.java:38
+    float newTrans = sqrt66 * dim;
+    for (int k = 0; k < 4; ++k) {  // up, front, left, right
+      push();
+      if (k == 0) translate(0, newTrans, 0);
+      else if (k == 1) sierp_shift(newTrans);
+      else if (k == 2) { rotate(120, 0, 1, 0); sierp_shift(newTrans); rotate(-120, 0, 1, 0); }
+      else { rotate(-120, 0, 1, 0); sierp_shift(newTrans); rotate(120, 0, 1, 0); }
+      scale(scVal, scVal, scVal);
+      if (!sierp_sub(newDim, scVal, name, level + 1, maxLevel, addShader)) return false;
+      pop();
+    }
+    return true;
+  }
+  void end_list(bool bvh) {  // endTmpObjList (myScene.java:305-324)
+    inList = false;
+    rt_accel_desc a;
+    std::memset(&a, 0, sizeof(a));
+    a.type = bvh ? 1 : 0;
+    a.first = (int)members.size();
+    a.count = (int)tmp.size();
+    put_ctm(a.ctm);
+    members.insert(members.end(), tmp.begin(), tmp.end());
+    top.push_back(~(int32_t)accels.size());
+    accels.push_back(a);
+    tmp.clear();
+    lastWasLight = false;
   }
   rt_prim_desc new_prim(int type) {
     rt_prim_desc p;
@@ -278,6 +375,7 @@ struct CliLoader {
           }
           L.color[0] = col.r; L.color[1] = col.g; L.color[2] = col.b;
           lights.push_back(L);
+          lastWasLight = true;
         } else if (c == "caustic_photons" || c == "diffuse_photons") {  // setPhotonHandling :919-931
           photonMap = true;
           caustic = (c.find("caustic") != std::string::npos);
@@ -315,18 +413,31 @@ struct CliLoader {
         } else if (c == "depth") {
         } else if (c == "begin_list") {
           inList = true; tmp.clear();
-        } else if (c == "end_list" || c == "end_accel") {  // endTmpObjList (myScene.java:305-324)
-          inList = false;
-          rt_accel_desc a;
-          std::memset(&a, 0, sizeof(a));
-          a.type = (c == "end_accel") ? 1 : 0;
-          a.first = (int)members.size();
-          a.count = (int)tmp.size();
-          put_ctm(a.ctm);
-          members.insert(members.end(), tmp.begin(), tmp.end());
-          top.push_back(~(int32_t)accels.size());
-          accels.push_back(a);
-          tmp.clear();
+        } else if (c == "end_list" || c == "end_accel") {
+          end_list(c == "end_accel");
+        } else if (c == "named_object") {  // setObjectAsNamedObject (myScene.java:378-387)
+          if (inList || top.empty() || lastWasLight) { err = "named_object: only a scene object (not a light) can be named"; return false; }
+          int32_t v = top.back();
+          if (v >= 0 && (v & RT_REF_INSTANCE)) { err = "named_object of an instance is unsupported"; return false; }
+          top.pop_back();
+          named[t.at(1)] = v;
+        } else if (c == "instance") {  // myRTFileReader.java:250-256: any 3rd token selects the current shader
+          if (!add_instance(t.at(1), t.size() > 2)) return false;
+        } else if (c == "sierpinski") {  // myRTFileReader.java:234-241, buildSierpinski (myScene.java:371-377)
+          std::string objName = t.at(1);
+          float sc = .5f;
+          int depth = 5;
+          bool useShdr = false;  // useShdr != "No": true iff a 5th token was parsed
+          try {
+            depth = std::stoi(t.at(2));
+            sc = std::stof(t.at(3));
+            useShdr = t.size() > 4;
+          } catch (...) {
+          }
+          if (inList) { err = "sierpinski inside begin_list is unsupported"; return false; }
+          inList = true; tmp.clear();  // startTmpObjList
+          if (!sierp_sub(8, sc, objName, 0, depth, useShdr)) return false;
+          end_list(true);
         } else if (c == "texture" || c == "image_texture") {  // :257-273
           std::string lo = t.at(1);
           for (auto& ch : lo) ch = (char)std::tolower(ch);
@@ -435,31 +546,16 @@ struct CliLoader {
           for (int i = 0; i < 4; ++i) p.p[i] = num(t, 1 + i);
           p.nverts = 4;
           add_prim(p);
-        } else if (c == "push") {  // gtPushMatrix :1241-1246
-          stack.push_back(stack.back());
+        } else if (c == "push") {
+          push();
         } else if (c == "pop") {
-          if (stack.size() > 1) stack.pop_back();
-        } else if (c == "translate") {  // :1256-1264
-          Mat T = Mat::ident();
-          T.m[3] = num(t, 1); T.m[7] = num(t, 2); T.m[11] = num(t, 3);
-          stack.back() = mul(stack.back(), T);
+          pop();
+        } else if (c == "translate") {
+          translate(num(t, 1), num(t, 2), num(t, 3));
         } else if (c == "scale") {
-          Mat S = Mat::ident();
-          S.m[0] = num(t, 1); S.m[5] = num(t, 2); S.m[10] = num(t, 3);
-          stack.back() = mul(stack.back(), S);
-        } else if (c == "rotate") {  // gtRotate :1280-1318
-          double ang = num(t, 1), ax = num(t, 2), ay = num(t, 3), az = num(t, 4);
-          double ar = (double)(ang * M_PI) / 180.0;
-          D3 av = normalized(d3(ax, ay, az));
-          D3 nv = (ax == 0) ? d3(1, 0, 0) : d3(0, 1, 0);
-          D3 bv = normalized(cross(av, nv));
-          D3 cv = normalized(cross(av, bv));
-          Mat R1 = Mat::ident(), R2 = Mat::ident();
-          R1.m[0] = av.x; R1.m[1] = av.y; R1.m[2] = av.z;
-          R1.m[4] = bv.x; R1.m[5] = bv.y; R1.m[6] = bv.z;
-          R1.m[8] = cv.x; R1.m[9] = cv.y; R1.m[10] = cv.z;
-          R2.m[5] = std::cos(ar); R2.m[6] = -std::sin(ar); R2.m[9] = std::sin(ar); R2.m[10] = std::cos(ar);
-          stack.back() = mul(stack.back(), mul(transpose(R1), mul(R2, R1)));
+          scale(num(t, 1), num(t, 2), num(t, 3));
+        } else if (c == "rotate") {
+          rotate(num(t, 1), num(t, 2), num(t, 3), num(t, 4));
         } else if (c == "reset_timer" || c == "print_timer" || c == "refine") {
           // timers and progressive `refine` are outside the kernel path (documented override)
         } else {
@@ -500,6 +596,7 @@ static int load_desc(const char* scene_dir, const char* cli_file, int num_textur
   d.num_lights = (int)L.lights.size(); d.lights = L.lights.data();
   d.num_accels = (int)L.accels.size(); d.accels = L.accels.data(); d.accel_members = L.members.data();
   d.num_top = (int)L.top.size(); d.top = L.top.data();
+  d.num_instances = (int)L.insts.size(); d.instances = L.insts.data();
   d.num_textures = num_textures; d.textures = textures;
   return RT_OK;
 }

@@ -28,14 +28,20 @@ struct TriD {
 };
 
 enum : int32_t {
-  PT_TRI = 0, PT_QUAD = 1, PT_PLANE = 2, PT_SPHERE = 3, PT_MSPHERE = 4, PT_CYL = 5, PT_HCYL = 6, PT_BOX = 7
+  PT_TRI = 0, PT_QUAD = 1, PT_PLANE = 2, PT_SPHERE = 3, PT_MSPHERE = 4, PT_CYL = 5, PT_HCYL = 6, PT_BOX = 7,
+  PT_INST = 8  // myInstance: never tested itself (trace_kernels.h inst_closest / inst_any)
 };
+// PrimD.flags
+enum : int32_t { PF_INVERTED = 1, PF_INST_ACCEL = 2 };
 
 // Every other primitive, 256 B. Field use by type:
 //  QUAD/PLANE: a[0..11] v[4][3], a[12..14] NA, a[15..17] NB, a[18] DA, a[19] DB, a[20..27] uv[4][2]
 //  SPHERE/MSPHERE: a[0..2] origin (origin0), a[3..5] radii, a[6..8] origin1
 //  CYL/HCYL: a[0..2] origin, a[3] radX, a[4] radZ, a[5] height, a[6] yTop, a[7] yBottom, a[8..15] caps
 //  BOX: a[0..2] min, a[3..5] max
+//  INST: xf = instance CTM, xfc = list CTM x instance CTM when inside an accel (else -1),
+//        mat = instance shader or -1, pad[0] = named object (PF_INST_ACCEL: accel index,
+//        else its tri/prim ref)
 struct PrimD {
   int32_t type, xf, xfc, mat;
   uint32_t key;
@@ -69,7 +75,7 @@ struct AccelD {
   int32_t is_list;   // end_list
   int32_t pad;
 };
-enum : int32_t { TOP_TRI = 0, TOP_PRIM = 1, TOP_ACCEL = 2 };
+enum : int32_t { TOP_TRI = 0, TOP_PRIM = 1, TOP_ACCEL = 2, TOP_INST = 3 };  // TOP_INST: idx = PT_INST prim
 struct TopD {
   int32_t kind, idx, xf;
   uint32_t key;

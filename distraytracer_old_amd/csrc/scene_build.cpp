@@ -65,9 +65,12 @@ struct Builder {
   const rt_scene_desc* d;
   HostScene& hs;
   std::map<std::string, int> xfIndex;
-  std::vector<int32_t> ref;      // desc prim -> encoded ref (>=0 tri, <0 ~prim)
-  std::vector<D3> transOrigin;   // desc prim -> CTM * origin
-  std::vector<Box> objBox;       // desc prim -> object-space bbox (_bbox)
+  // object ids: desc prim i -> i, desc instance j -> num_prims + j
+  std::vector<int32_t> ref;      // object -> encoded ref (>=0 tri, <0 ~prim; instances are PT_INST prims)
+  std::vector<D3> transOrigin;   // object -> CTM * origin
+  std::vector<Box> objBox;       // object -> object-space bbox (_bbox)
+  std::vector<char> boxReady;    // instance boxes are formed when an accel first needs them
+  std::vector<char> accHasInst, instUsed;
   std::string err;
 
   Builder(const rt_scene_desc* dd, HostScene& h) : d(dd), hs(h) {}
@@ -223,6 +226,72 @@ struct Builder {
     hs.prim.push_back(q);
     ref[i] = ~(int32_t)(hs.prim.size() - 1);
   }
+  const double* obj_ctm(int id) const {
+    return id < d->num_prims ? d->prims[id].ctm : d->instances[id - d->num_prims].ctm;
+  }
+  // desc member / top entry -> object id (-1: out of range)
+  int obj_id(int32_t m) const {
+    if (m >= 0 && (m & RT_REF_INSTANCE)) {
+      int j = m & ~RT_REF_INSTANCE;
+      return j < d->num_instances ? d->num_prims + j : -1;
+    }
+    return (m >= 0 && m < d->num_prims) ? m : -1;
+  }
+  // myInstance (mySceneObject.java:98-110): a PT_INST prim naming the object
+  bool build_instance(int j) {
+    const rt_instance_desc& in = d->instances[j];
+    PrimD q;
+    std::memset(&q, 0, sizeof(q));
+    q.type = PT_INST;
+    q.xf = xf_id(ctm_of(in.ctm));
+    q.xfc = -1;
+    if (in.material < -1 || in.material >= d->num_materials) { err = "instance: bad material index"; return false; }
+    q.mat = in.material;
+    if (in.base >= 0) {
+      if (in.base >= d->num_prims) { err = "instance: base prim out of range"; return false; }
+      int ty = d->prims[in.base].type;
+      if (ty != RT_PRIM_TRIANGLE && ty != RT_PRIM_QUAD && ty != RT_PRIM_SPHERE && ty != RT_PRIM_CYLINDER &&
+          ty != RT_PRIM_HOLLOW_CYLINDER) {
+        err = "instance: unsupported named primitive (plane / box / moving sphere)";
+        return false;
+      }
+      q.pad[0] = ref[in.base];
+      q.key = (uint32_t)in.base;
+    } else {
+      int ai = ~in.base;
+      if (ai >= d->num_accels) { err = "instance: base accel out of range"; return false; }
+      q.flags = PF_INST_ACCEL;
+      q.pad[0] = ai;
+    }
+    hs.prim.push_back(q);
+    const int id = d->num_prims + j;
+    ref[id] = ~(int32_t)(hs.prim.size() - 1);
+    transOrigin[id] = d3(in.origin[0], in.origin[1], in.origin[2]);
+    return true;
+  }
+  // the instance's _bbox: named object's getMin/MaxVec through its own CTM (mySceneObject.java:104-113)
+  bool instance_box(int id, int curAccel) {
+    if (boxReady[id]) return true;
+    const rt_instance_desc& in = d->instances[id - d->num_prims];
+    Box base;
+    if (in.base >= 0) {
+      base = objBox[in.base];
+    } else {
+      int ai = ~in.base;
+      if (ai >= curAccel) { err = "instance of an accel defined later"; return false; }
+      if (accHasInst[ai]) { err = "instance of an accel holding instances is unsupported"; return false; }
+      const AccelD& a = hs.accel[ai];
+      for (int c = 0; c < 3; ++c) { base.mn[c] = a.bmin[c]; base.mx[c] = a.bmax[c]; }
+    }
+    Mat bg = ctm_of(in.base >= 0 ? d->prims[in.base].ctm : d->accels[~in.base].ctm);
+    D3 mn = xform(bg, d3(base.mn[0], base.mn[1], base.mn[2]), 1), mx = xform(bg, d3(base.mx[0], base.mx[1], base.mx[2]), 1);
+    double a[3] = {mn.x, mn.y, mn.z}, b[3] = {mx.x, mx.y, mx.z};
+    Box bb;
+    calc_min_max(bb, a, b);
+    objBox[id] = bb;
+    boxReady[id] = 1;
+    return true;
+  }
   void set_xfc(int i, int xfc) {
     int32_t r = ref[i];
     if (r >= 0) hs.tri[r].xfc = xfc;
@@ -249,7 +318,7 @@ struct Builder {
       lf.start = (int)hs.member.size();
       lf.count = (int)lists[0].size();
       for (int p : lists[0]) {
-        Mat tmp = mul(accInv, ctm_of(d->prims[p].ctm));
+        Mat tmp = mul(accInv, ctm_of(obj_ctm(p)));
         expand_box(lb, objBox[p], &tmp);
         hs.member.push_back(ref[p]);
       }
@@ -303,10 +372,17 @@ struct Builder {
     std::memset(&ad, 0, sizeof(ad));
     ad.xf = axf;
     ad.is_list = (a.type == 0);
-    std::vector<int> mem(d->accel_members + a.first, d->accel_members + a.first + a.count);
-    for (int p : mem) {
-      if (p < 0 || p >= d->num_prims) { err = "accel member out of range"; return false; }
-      set_xfc(p, xf_id(mul(g, ctm_of(d->prims[p].ctm))));  // reBuildCTMara(objCTM, accelCTM)
+    std::vector<int> mem;
+    for (int k = 0; k < a.count; ++k) {
+      int id = obj_id(d->accel_members[a.first + k]);
+      if (id < 0) { err = "accel member out of range"; return false; }
+      if (id >= d->num_prims) {
+        if (instUsed[id - d->num_prims]++) { err = "instance listed twice"; return false; }
+        if (!instance_box(id, ai)) return false;
+        accHasInst[ai] = 1;
+      }
+      mem.push_back(id);
+      set_xfc(id, xf_id(mul(g, ctm_of(obj_ctm(id)))));  // reBuildCTMara(objCTM, accelCTM)
     }
     Box box;
     if (a.type == 0) {  // myGeomList: one leaf in insertion order, its own box
@@ -314,7 +390,7 @@ struct Builder {
       lf.start = (int)hs.member.size();
       lf.count = (int)mem.size();
       for (int p : mem) {
-        Mat tmp = mul(inv, ctm_of(d->prims[p].ctm));
+        Mat tmp = mul(inv, ctm_of(obj_ctm(p)));
         expand_box(box, objBox[p], &tmp);
         hs.member.push_back(ref[p]);
       }
@@ -332,14 +408,22 @@ struct Builder {
 
   bool run() {
     int n = d->num_prims;
-    ref.assign(n, 0);
-    transOrigin.assign(n, d3(0, 0, 0));
-    objBox.assign(n, Box());
+    const int ni = d->num_instances;
+    if (ni < 0 || (ni > 0 && !d->instances)) { err = "bad instance list"; return false; }
+    ref.assign(n + ni, 0);
+    transOrigin.assign(n + ni, d3(0, 0, 0));
+    objBox.assign(n + ni, Box());
+    boxReady.assign(n + ni, 1);
+    for (int j = 0; j < ni; ++j) boxReady[n + j] = 0;
+    accHasInst.assign(d->num_accels, 0);
+    instUsed.assign(ni, 0);
     hs.nprims = n;
     for (int i = 0; i < n; ++i) {
       if (d->prims[i].material < 0 || d->prims[i].material >= d->num_materials) { err = "bad material index"; return false; }
       if (!build_prim(i)) return false;
     }
+    for (int j = 0; j < ni; ++j)
+      if (!build_instance(j)) return false;
     for (int a = 0; a < d->num_accels; ++a)
       if (!build_accel(a)) return false;
     if (hs.bvhDepth > 40) { err = "BVH deeper than the kernel traversal stack (40)"; return false; }
@@ -347,7 +431,20 @@ struct Builder {
       int32_t t = d->top[k];
       TopD td;
       std::memset(&td, 0, sizeof(td));
-      if (t >= 0) {
+      if (t >= 0 && (t & RT_REF_INSTANCE)) {
+        int id = obj_id(t);
+        if (id < 0) { err = "top instance out of range"; return false; }
+        if (instUsed[id - n]++) { err = "instance listed twice"; return false; }
+        const PrimD& q = hs.prim[~ref[id]];
+        if ((q.flags & PF_INST_ACCEL) && accHasInst[q.pad[0]]) {
+          err = "instance of an accel holding instances is unsupported";
+          return false;
+        }
+        td.kind = TOP_INST;
+        td.idx = ~ref[id];
+        td.xf = q.xf;
+        td.key = q.key;
+      } else if (t >= 0) {
         if (t >= n) { err = "top object out of range"; return false; }
         int32_t r = ref[t];
         td.kind = r >= 0 ? TOP_TRI : TOP_PRIM;
@@ -489,6 +586,8 @@ void pack_leaves(HostScene& hs) {
     if (r >= 0) r = perm[r];
   for (TopD& t : hs.top)
     if (t.kind == TOP_TRI) t.idx = perm[t.idx];
+  for (PrimD& q : hs.prim)  // instanced triangles
+    if (q.type == PT_INST && !(q.flags & PF_INST_ACCEL) && q.pad[0] >= 0) q.pad[0] = perm[q.pad[0]];
   // child references of leaves that are consecutive triangle runs
   auto code = [&](int32_t child) -> int32_t {
     if (child >= 0) return child;

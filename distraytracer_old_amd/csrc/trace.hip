@@ -246,6 +246,8 @@ static int make_params(rt_scene* s, const rt_render_params* p, ParamsD& P) {
 static uint32_t scene_features(const HostScene& h) {
   uint32_t f = 0;
   if (!h.prim.empty()) f |= dv::FT_PRIM;
+  for (const PrimD& q : h.prim)
+    if (q.type == PT_INST) { f |= dv::FT_INST; break; }
   if (h.bkgTex >= 0) f |= dv::FT_TEX;
   if (h.photonMode) f |= dv::FT_PHOTON;
   if (h.dof) f |= dv::FT_DOF;
@@ -273,6 +275,8 @@ static const Variant kVariants[] = {
      dv::render_kernel<false, dv::FT_PRIM | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX>},
     {dv::FT_PRIM | dv::FT_TRANS | dv::FT_PHOTON | dv::FT_LIGHTX,
      dv::render_kernel<false, dv::FT_PRIM | dv::FT_TRANS | dv::FT_PHOTON | dv::FT_LIGHTX>},
+    {dv::FT_PRIM | dv::FT_INST | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX,
+     dv::render_kernel<false, dv::FT_PRIM | dv::FT_INST | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX>},
     {dv::FT_ALL, dv::render_kernel<false, dv::FT_ALL>},
 };
 
@@ -444,8 +448,13 @@ static int shoot_photons(rt_scene* s, uint64_t seed, int64_t first, int64_t coun
   std::vector<dv::PhotonOut> out((size_t)dv::PH_SLOTS * CH);
   for (long base = 0; base < total && e == hipSuccess; base += CH) {
     const long n = std::min(CH, total - base);
-    hipLaunchKernelGGL(dv::photon_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), dv::LDS_BYTES, 0, s->dev, seed,
-                       (long)first, (long)count, base, n, caustic ? 1 : 0, pwrMult, d_out, d_cnt);
+    if (scene_features(h) & dv::FT_INST)
+      hipLaunchKernelGGL(dv::photon_kernel<dv::FT_ALL>, dim3((unsigned)((n + 63) / 64)), dim3(64), dv::LDS_BYTES, 0,
+                         s->dev, seed, (long)first, (long)count, base, n, caustic ? 1 : 0, pwrMult, d_out, d_cnt);
+    else
+      hipLaunchKernelGGL(dv::photon_kernel<dv::FT_ALL & ~dv::FT_INST>, dim3((unsigned)((n + 63) / 64)), dim3(64),
+                         dv::LDS_BYTES, 0, s->dev, seed, (long)first, (long)count, base, n, caustic ? 1 : 0, pwrMult,
+                         d_out, d_cnt);
     e = hipGetLastError();
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(cnt.data(), d_cnt, sizeof(int) * n, hipMemcpyDeviceToHost);

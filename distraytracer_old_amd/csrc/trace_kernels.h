@@ -26,7 +26,8 @@ enum : uint32_t {
   FT_DOF = 16,    // lens / depth of field
   FT_LIGHTX = 32, // spot or disk lights
   FT_CAMX = 64,   // fisheye or orthographic camera
-  FT_ALL = 127
+  FT_INST = 128,  // instances (named_object / instance / sierpinski)
+  FT_ALL = 255
 };
 
 __constant__ int c_perm[256];
@@ -38,11 +39,19 @@ __constant__ int c_grad3[12][3];
 struct Best {
   double t;
   int32_t ref;   // >= 0 tri, < 0 ~prim
-  uint32_t ver;  // direction version at the winning test
+  uint32_t ver;  // world-ray direction version at the winning test (at the instance entry for instance hits)
   int16_t top;   // objList index
   int16_t inAcc; // hit came from an accel structure (reCalcCTMHitNorm applies)
+  int32_t inst;  // PT_INST prim the hit came through, -1 none
+  uint32_t iver; // instance-ray direction version at the winning test
 };
-DEVI Best miss() { Best b; b.t = DMAX; b.ref = 0; b.top = -1; b.ver = 0; b.inAcc = 0; return b; }
+DEVI Best miss() { Best b; b.t = DMAX; b.ref = 0; b.top = -1; b.ver = 0; b.inAcc = 0; b.inst = -1; b.iver = 0; return b; }
+// what a leaf records with a hit: objList entry, instance (or -1) and the world-ray version
+// at the instance's entry (the traced ray's own version otherwise)
+struct HitCtx {
+  int32_t top, inst;
+  uint32_t wver;
+};
 
 template <bool CNT, uint32_t F, class LIM = LimNone>
 DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, double& t, int& args, Counters& ct,
@@ -57,6 +66,8 @@ DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, double&
 }
 template <uint32_t F>
 DEVI int32_t ref_xf(const SceneD& S, int32_t ref) { return (!(F & FT_PRIM) || ref >= 0) ? S.tri[ref].xf : S.prim[~ref].xf; }
+template <uint32_t F>
+DEVI bool is_inst(const SceneD& S, int32_t ref) { return (F & FT_INST) && ref < 0 && S.prim[~ref].type == PT_INST; }
 
 // The reference returns a best hit per BVH node and merges children keeping the first of
 // equal t (TreeMap); over the whole scan that is "the first-visited hit of minimal t", so
@@ -64,7 +75,6 @@ DEVI int32_t ref_xf(const SceneD& S, int32_t ref) { return (!(F & FT_PRIM) || re
 // the per-node results are still needed for is the pruning rule (below), which only
 // needs each subtree's minimal t -- a double per stack frame.
 
-// myGeomList.traverseStruct leaf loop (myGeomBase.java:281-296): strict <, leaf order
 // a leaf from its child code c = ~ref (rt_types.h): a LeafD or a packed triangle run
 struct LeafR {
   int32_t start, count;
@@ -80,13 +90,25 @@ DEVI LeafR leaf_of(const SceneD& S, int32_t c) {
 DEVI int32_t leaf_member(const SceneD& S, const LeafR& lf, int i) { return lf.run ? lf.start + i : S.member[lf.start + i]; }
 
 template <bool CNT, uint32_t F>
-DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w, const Key& k, int top, Best& best,
-                       double& local, Counters& ct) {
+DEVI void inst_closest(const SceneD& S, int32_t ii, WRay& w, const Key& k, int top, Best& best, double& local, Counters& ct);
+
+// myGeomList.traverseStruct leaf loop (myGeomBase.java:281-296): strict <, leaf order.
+// w is the leaf's `_ray`: the world ray, or (INST) the instance ray of an instanced accel;
+// accXf >= 0: members with that CTM reuse the accel-space ray (ao, ad) while w is unchanged.
+template <bool CNT, uint32_t F, bool INST>
+DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w, const Key& k, const HitCtx& hc,
+                       Best& best, double& local, Counters& ct) {
   const LeafR lf = leaf_of(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
   for (int i = 0; i < lf.count; ++i) {
     int32_t ref = leaf_member(S, lf, i);
     renorm(w);  // _ray.getTransformedRay(_ray, obj.CTMara[invIDX])
+    if constexpr (!INST && (F & FT_INST) != 0) {
+      if (is_inst<F>(S, ref)) {  // a sierpinski element: myInstance.intersectCheck
+        inst_closest<CNT, F>(S, ~ref, w, k, hc.top, best, local, ct);
+        continue;
+      }
+    }
     int xf = ref_xf<F>(S, ref);
     V o, d;
     if (xf == accXf && !w.moved) { o = ao; d = ad; }
@@ -95,16 +117,22 @@ DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRa
     int args;
     if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, LimClosest{local, best.t})) {
       if (t < local) local = t;
-      if (t < best.t) { best.t = t; best.ref = ref; best.ver = w.ver; best.top = (int16_t)top; best.inAcc = 1; }
+      if (t < best.t) {
+        best.t = t; best.ref = ref; best.top = (int16_t)hc.top; best.inAcc = 1; best.inst = hc.inst;
+        if (INST) { best.ver = hc.wver; best.iver = w.ver; }
+        else { best.ver = w.ver; best.iver = 0; }
+      }
     }
   }
 }
 
 static constexpr int BVH_STACK = 40;  // host rejects BVHs deeper than 40
 
-// Traversal stacks: the first STK_LDS levels live in LDS ([level][lane], conflict-free),
+// Traversal stacks: the first NL levels live in LDS ([level][lane], conflict-free),
 // deeper levels in scratch. The closest-hit and shadow traversals never overlap in time,
-// so they share the LDS node-index array. One wave per workgroup.
+// so they share the LDS node-index array. One wave per workgroup. The traversal of an
+// instanced accel runs while the enclosing one is suspended: it keeps its whole stack in
+// scratch (NL = 0).
 #ifndef RT_STACK_LDS
 #define RT_STACK_LDS 12
 #endif
@@ -118,48 +146,54 @@ typedef __attribute__((address_space(3))) double lds_f64;
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 DEVI lds_f64* ldsT() { return (lds_f64*)rt_lds; }
 DEVI lds_i32* ldsN() { return (lds_i32*)(rt_lds + STK_LDS * 64); }
-struct Stack {
-  double sT[BVH_STACK - STK_LDS];
-  int32_t sN[BVH_STACK - STK_LDS];
+template <int NL>
+struct StackT {
+  double sT[BVH_STACK - NL];
+  int32_t sN[BVH_STACK - NL];
   DEVI double getT(int i) const {
-    if (i < STK_LDS) return ldsT()[i * 64 + threadIdx.x];
-    return sT[i - STK_LDS];
+    if (NL > 0 && i < NL) return ldsT()[i * 64 + threadIdx.x];
+    return sT[i - NL];
   }
   DEVI void setT(int i, double v) {
-    if (i < STK_LDS) ldsT()[i * 64 + threadIdx.x] = v;
-    else sT[i - STK_LDS] = v;
+    if (NL > 0 && i < NL) ldsT()[i * 64 + threadIdx.x] = v;
+    else sT[i - NL] = v;
   }
   DEVI int32_t getN(int i) const {
-    if (i < STK_LDS) return ldsN()[i * 64 + threadIdx.x];
-    return sN[i - STK_LDS];
+    if (NL > 0 && i < NL) return ldsN()[i * 64 + threadIdx.x];
+    return sN[i - NL];
   }
   DEVI void setN(int i, int32_t v) {
-    if (i < STK_LDS) ldsN()[i * 64 + threadIdx.x] = v;
-    else sN[i - STK_LDS] = v;
+    if (NL > 0 && i < NL) ldsN()[i * 64 + threadIdx.x] = v;
+    else sN[i - NL] = v;
   }
 };
+typedef StackT<STK_LDS> Stack;
 
-struct NStack {  // shadow traversal: node indices only
-  int32_t sN[BVH_STACK - STK_LDS];
+template <int NL>
+struct NStackT {  // shadow traversal: node indices only
+  int32_t sN[BVH_STACK - NL];
   DEVI int32_t getN(int i) const {
-    if (i < STK_LDS) return ldsN()[i * 64 + threadIdx.x];
-    return sN[i - STK_LDS];
+    if (NL > 0 && i < NL) return ldsN()[i * 64 + threadIdx.x];
+    return sN[i - NL];
   }
   DEVI void setN(int i, int32_t v) {
-    if (i < STK_LDS) ldsN()[i * 64 + threadIdx.x] = v;
-    else sN[i - STK_LDS] = v;
+    if (NL > 0 && i < NL) ldsN()[i * 64 + threadIdx.x] = v;
+    else sN[i - NL] = v;
   }
 };
+typedef NStackT<STK_LDS> NStack;
 
 // myAccelStruct.intersectCheck + myBVH.traverseStruct (myGeomBase.java:216-222, 407-421),
 // iteratively with the reference's LOCAL pruning: the right child is visited iff its
 // box is hit and (left subtree missed or box entry t < the LEFT SUBTREE's minimal t);
 // ties go left. A frame = the enclosing subtree's minimal t so far + node<<1|phase; the
 // right box is tested when the left subtree is done, as the Java does.
-template <bool CNT, uint32_t F>
-DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, const RayInv& ri, WRay& w, const Key& k, int top,
-                        Best& best, Counters& ct) {
-  Stack st;
+// INST: an instanced accel, whose `_ray` and `_trans` are the same ray object: the boxes
+// are tested with w itself, re-normalised in place by the leaves (myInstance.intersectCheck).
+template <bool CNT, uint32_t F, bool INST>
+DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, RayInv ri, WRay& w, const Key& k,
+                        const HitCtx& hc, Best& best, double& outer, Counters& ct) {
+  StackT<INST ? 0 : STK_LDS> st;
   int sp = 0;
   double local = DMAX;
   int32_t N = A.root;  // a leaf root (a plain list) is tested by the same loop with no frames
@@ -175,7 +209,10 @@ DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, const RayI
       if (box_hit(nd.lmin, nd.lmax, ao, ad, ri)) N = nd.left;
       else { N = INT32_MAX; break; }
     }
-    if (N != INT32_MAX) leaf_closest<CNT, F>(S, ~N, A.xf, ao, ad, w, k, top, best, local, ct);
+    if (N != INT32_MAX) {
+      leaf_closest<CNT, F, INST>(S, ~N, INST ? -1 : A.xf, ao, ad, w, k, hc, best, local, ct);
+      if (INST && w.moved) { ad = w.d; ri = ray_inv(ao, ad, S.fastSlab); w.moved = false; }
+    }
     // unwind
     N = INT32_MAX;
     while (sp > 0) {
@@ -195,6 +232,43 @@ DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, const RayI
     }
     if (N == INT32_MAX) break;
   }
+  if (local < outer) outer = local;
+}
+
+// myInstance.intersectCheck (mySceneObject.java:119-124): the named object tested with
+// the instance ray (instance CTM inverse x w) as both of its rays; for a named accel
+// that ray is re-normalised in place by its leaves. `local` receives the minimal t.
+template <bool CNT, uint32_t F>
+DEVI void inst_closest(const SceneD& S, int32_t ii, WRay& w, const Key& k, int top, Best& best, double& local,
+                       Counters& ct) {
+  if constexpr ((F & FT_INST) != 0) {
+    const PrimD& I = S.prim[ii];
+    const double* inv = S.xf[I.xf].inv;
+    WRay wi;
+    wi.o = xpt(inv, w.o);
+    wi.d = xvec(inv, w.d);
+    wi.d0 = wi.d;
+    wi.ver = 0; wi.stable = false; wi.moved = false;
+    const HitCtx hc{top, ii, w.ver};
+    if (I.flags & PF_INST_ACCEL) {
+      const AccelD& A = S.accel[I.pad[0]];
+      if (CNT) { ct.c[C_ROOT]++; ct.c[C_BOX]++; }
+      const RayInv ri = ray_inv(wi.o, wi.d, S.fastSlab);
+      if (!box_hit(A.bmin, A.bmax, wi.o, wi.d, ri)) return;  // myAccelStruct.intersectCheck root box
+      accel_closest<CNT, F, true>(S, A, wi.o, wi.d, ri, wi, k, hc, best, local, ct);
+    } else {
+      double t;
+      int args;
+      const int32_t ref = I.pad[0];
+      if (test_ref<CNT, F>(S, ref, wi.o, wi.d, k, t, args, ct, LimClosest{local, best.t})) {
+        if (t < local) local = t;
+        if (t < best.t) {
+          best.t = t; best.ref = ref; best.top = (int16_t)top; best.inAcc = 0; best.inst = ii;
+          best.ver = w.ver; best.iver = 0;
+        }
+      }
+    }
+  }
 }
 
 // findClosestRayHit (myScene.java:888-903): objList scan, TreeMap keeps the first of equal t
@@ -205,6 +279,11 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
     TopD tp = S.top[i];
     if (CNT) ct.c[C_TOP]++;
     renorm(w);
+    if ((F & FT_INST) && tp.kind == TOP_INST) {
+      double local = best.t;
+      inst_closest<CNT, F>(S, tp.idx, w, k, i, best, local, ct);
+      continue;
+    }
     const double* inv = S.xf[tp.xf].inv;
     V o = xpt(inv, w.o), d = xvec(inv, w.d);
     if (tp.kind == TOP_ACCEL) {
@@ -213,13 +292,14 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       RayInv ri = ray_inv(o, d, S.fastSlab);
       if (!box_hit(A.bmin, A.bmax, o, d, ri)) continue;
       w.moved = false;
-      accel_closest<CNT, F>(S, A, o, d, ri, w, k, i, best, ct);
+      double local = DMAX;
+      accel_closest<CNT, F, false>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
     } else {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
       int args;
       if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, LimClosest{best.t, best.t}) && t < best.t) {
-        best.t = t; best.ref = ref; best.top = (int16_t)i; best.inAcc = 0; best.ver = w.ver;
+        best.t = t; best.ref = ref; best.top = (int16_t)i; best.inAcc = 0; best.ver = w.ver; best.inst = -1; best.iver = 0;
       }
     }
   }
@@ -234,12 +314,21 @@ DEVI bool shadow_box(const double* mn, const double* mx, V o, V d, const RayInv&
   return box_shadow(mn, mx, o, d, ri, dist);
 }
 template <bool CNT, uint32_t F>
+DEVI bool inst_any(const SceneD& S, int32_t ii, const WRay& w, const Key& k, double dist, Counters& ct);
+
+template <bool CNT, uint32_t F, bool INST>
 DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
   const LeafR lf = leaf_of(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
   for (int i = 0; i < lf.count; ++i) {
     int32_t ref = leaf_member(S, lf, i);
     renorm(w);
+    if constexpr (!INST && (F & FT_INST) != 0) {
+      if (is_inst<F>(S, ref)) {  // myInstance.calcShadowHit
+        if (inst_any<CNT, F>(S, ~ref, w, k, dist, ct)) return true;
+        continue;
+      }
+    }
     int xf = ref_xf<F>(S, ref);
     V o, d;
     if (xf == accXf && !w.moved) { o = ao; d = ad; }
@@ -250,10 +339,10 @@ DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w
   }
   return false;
 }
-template <bool CNT, uint32_t F>
+template <bool CNT, uint32_t F, bool INST>
 DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
-  const RayInv ri = ray_inv(ao, ad, S.fastSlab);
-  NStack st;
+  RayInv ri = ray_inv(ao, ad, S.fastSlab);
+  NStackT<INST ? 0 : STK_LDS> st;
   int sp = 0;
   int32_t N = A.root;
   // leafVals.calcShadowHit tests its own box first; myBVH.calcShadowHit (internal) does not
@@ -265,7 +354,8 @@ DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const
       st.setN(sp++, N);
       if (shadow_box<CNT>(nd.lmin, nd.lmax, ao, ad, ri, dist, ct)) { N = nd.left; continue; }
     } else if (N != INT32_MAX) {
-      if (leaf_any<CNT, F>(S, ~N, A.xf, ao, ad, w, k, dist, ct)) return true;
+      if (leaf_any<CNT, F, INST>(S, ~N, INST ? -1 : A.xf, ao, ad, w, k, dist, ct)) return true;
+      if (INST && w.moved) { ad = w.d; ri = ray_inv(ao, ad, S.fastSlab); w.moved = false; }
     }
     N = INT32_MAX;
     while (sp > 0) {
@@ -275,6 +365,24 @@ DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const
     if (N == INT32_MAX) return false;
   }
 }
+// myInstance.calcShadowHit (mySceneObject.java:115-118): obj.calcShadowHit(_trans, _trans, ...)
+template <bool CNT, uint32_t F>
+DEVI bool inst_any(const SceneD& S, int32_t ii, const WRay& w, const Key& k, double dist, Counters& ct) {
+  if constexpr ((F & FT_INST) != 0) {
+    const PrimD& I = S.prim[ii];
+    const double* inv = S.xf[I.xf].inv;
+    WRay wi;
+    wi.o = xpt(inv, w.o);
+    wi.d = xvec(inv, w.d);
+    wi.d0 = wi.d;
+    wi.ver = 0; wi.stable = false; wi.moved = false;
+    if (I.flags & PF_INST_ACCEL) return accel_any<CNT, F, true>(S, S.accel[I.pad[0]], wi.o, wi.d, wi, k, dist, ct);
+    double t;
+    int args;
+    return test_ref<CNT, F>(S, I.pad[0], wi.o, wi.d, k, t, args, ct, LimShadow{dist}) && (dist - t) > EPS;
+  }
+  return false;
+}
 // myScene.calcShadow (myScene.java:879-885)
 template <bool CNT, uint32_t F>
 DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters& ct) {
@@ -282,12 +390,16 @@ DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters
     TopD tp = S.top[i];
     if (CNT) ct.c[C_TOP]++;
     renorm(w);
+    if ((F & FT_INST) && tp.kind == TOP_INST) {
+      if (inst_any<CNT, F>(S, tp.idx, w, k, dist, ct)) return true;
+      continue;
+    }
     const double* inv = S.xf[tp.xf].inv;
     V o = xpt(inv, w.o), d = xvec(inv, w.d);
     if (tp.kind == TOP_ACCEL) {
       if (CNT) ct.c[C_ROOT]++;
       w.moved = false;
-      if (accel_any<CNT, F>(S, S.accel[tp.idx], o, d, w, k, dist, ct)) return true;
+      if (accel_any<CNT, F, false>(S, S.accel[tp.idx], o, d, w, k, dist, ct)) return true;
     } else {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
@@ -315,8 +427,23 @@ DEVI HitRec make_hit(const SceneD& S, const Best& b, const WRay& w, const Key& k
   if (!(F & FT_PRIM) || ref >= 0) { const TriD& T = S.tri[ref]; xf = T.xf; xfc = T.xfc; h.mat = T.mat; h.key = T.key; h.type = PT_TRI; }
   else { const PrimD& P = S.prim[~ref]; xf = P.xf; xfc = P.xfc; h.mat = P.mat; h.key = P.key; h.type = P.type; }
   h.ref = ref;
+  V ro = w.o;  // the ray the primitive's caller passed as `_ray` (its direction is rawRayDir)
+  int hitXf = -1;  // CTM of the hit record when it is not the primitive's own / accel one
+  bool direct = false;  // the primitive was tested with `ro, dw` itself (instanced primitive)
+  if ((F & FT_INST) && b.inst >= 0) {  // myInstance: the instance ray, re-normalised `iver` times
+    const PrimD& I = S.prim[b.inst];
+    const XformD& XI = S.xf[I.xf];
+    ro = xpt(XI.inv, w.o);
+    dw = xvec(XI.inv, dw);
+    for (uint32_t i = 0; i < b.iver; ++i) dw = nrmz(dw);
+    if (I.mat >= 0) h.mat = I.mat;  // useInstShader
+    direct = !(I.flags & PF_INST_ACCEL);
+    // reCalcCTMHitNorm by the list holding the instance (sierpinski), else the instance CTM
+    // (instanced primitive) or the named accel's leaf CTM (xfc, as for any accel hit)
+    hitXf = (I.xfc >= 0) ? I.xfc : (direct ? I.xf : -1);
+  }
   const XformD& X = S.xf[xf];
-  V tro = xpt(X.inv, w.o), trd = xvec(X.inv, dw);
+  V tro = direct ? ro : xpt(X.inv, ro), trd = direct ? dw : xvec(X.inv, dw);
   double t = b.t, tt;
   int args = 0;
   Counters dummy;
@@ -359,7 +486,7 @@ DEVI HitRec make_hit(const SceneD& S, const Best& b, const WRay& w, const Key& k
       }
     }
   }
-  const XformD& M = (b.inAcc && xfc >= 0) ? S.xf[xfc] : X;  // Q4: accel CTM x object CTM
+  const XformD& M = (hitXf >= 0) ? S.xf[hitXf] : (b.inAcc && xfc >= 0) ? S.xf[xfc] : X;  // Q4: accel CTM x object CTM
   h.fwd = xpt(M.g, p);
   h.nrm = nrmz(xvec(M.adj, n));
   h.dw = ((F & FT_PRIM) && h.type == PT_BOX) ? xvec(X.g, trd) : dw;
@@ -1539,10 +1666,11 @@ DEVI void new_wray(WRay& w, V o, V d) {
 
 // Lane gid of a launch covers photon (light li, index i) of the shard [first, first+count)
 // of every light, light-major: g = gBase + gid, li = g / count, i = first + g % count.
+// F: FT_ALL, or FT_ALL without FT_INST for scenes without instances
+template <uint32_t F>
 __global__ void __launch_bounds__(64) photon_kernel(SceneD S, uint64_t seed, long first, long count, long gBase,
                                                    long nLanes, int caustic, double pwrMult,
                                                    PhotonOut* __restrict__ out, int* __restrict__ cnt) {
-  constexpr uint32_t F = FT_ALL;
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= nLanes) return;
   const long g = gBase + gid;

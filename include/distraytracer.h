@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum rt_status {
   RT_OK = 0,
@@ -103,10 +103,22 @@ typedef struct rt_light_desc { /* myLight.java */
 
 typedef struct rt_accel_desc { /* myScene.endTmpObjList (myScene.java:305-324) */
   int32_t type;        /* 0 = end_list (myGeomList), 1 = end_accel (myBVH) */
-  int32_t first, count; /* range of rt_scene_desc.accel_members (prim indices, tmp-list order) */
+  int32_t first, count; /* range of rt_scene_desc.accel_members (prim indices or RT_INSTANCE_REF, tmp-list order) */
   int32_t pad;
   double ctm[16];      /* CTM when end_list/end_accel ran */
 } rt_accel_desc;
+
+/* myInstance (mySceneObject.java:95-145): `instance <name> [shdr]` of a `named_object`
+   (myScene.java:378-395), also the elements `sierpinski` lays out (myScene.java:339-377). */
+typedef struct rt_instance_desc {
+  int32_t base;      /* the named object: >= 0 prim index, < 0 ~accel index (an accel holding no instances) */
+  int32_t material;  /* instance shader (useInstShader), -1: the object's own shaders */
+  double ctm[16];    /* row-major: named object's CTM x matrix-stack top (buildCTMara, DistRayTracer.java:401) */
+  double origin[3];  /* trans_origin: matrix-stack top x (0,0,0) (myGeomBase ctor, myGeomBase.java:39) */
+} rt_instance_desc;
+/* rt_scene_desc.top / accel_members entry naming instance i */
+#define RT_REF_INSTANCE 0x40000000
+#define RT_INSTANCE_REF(i) (RT_REF_INSTANCE | (int32_t)(i))
 
 typedef struct rt_texture_desc {
   int32_t w, h;
@@ -124,7 +136,7 @@ typedef struct rt_scene_desc {
   const rt_accel_desc* accels;
   const int32_t* accel_members;
   int32_t num_top;
-  const int32_t* top; /* objList order: >= 0 prim index, < 0 accel ~index */
+  const int32_t* top; /* objList order: >= 0 prim index (or RT_INSTANCE_REF), < 0 accel ~index */
   int32_t num_textures;
   const rt_texture_desc* textures;
   double fov;            /* degrees */
@@ -139,6 +151,8 @@ typedef struct rt_scene_desc {
   int32_t photon_count, photon_k, pad1;
   double photon_max_dist; /* already rounded through float (Float.parseFloat) */
   double camera_param[2];  /* RT_CAMERA_FISHEYE: {aperture degrees, 0}; RT_CAMERA_ORTHO: {width, height} */
+  int32_t num_instances, pad2;
+  const rt_instance_desc* instances;
 } rt_scene_desc;
 
 /* rt_scene_desc.camera */

@@ -563,6 +563,8 @@ struct AccelStruct : GeomBase {
     return traverse(ray, tr, ctara, st);
   }
   V3 normalAt(const V3& p, const int* a) override { return bbox->normalAt(p, a); }
+  V3 getMaxVec() override { return bbox->maxVals; }  // :240-243
+  V3 getMinVec() override { return bbox->minVals; }
 };
 struct GeomList : AccelStruct {  // :251-306
   std::vector<GeomBase*> objs;
@@ -597,7 +599,7 @@ struct GeomList : AccelStruct {  // :251-306
     if (clsObj->isAccel()) {  // nested accel (not on the config path)
       return static_cast<AccelStruct*>(clsObj)->traverse(ray, clsTr, cls.ctm, st);
     }
-    V3 n = clsObj->normalAt(cls.hitLoc, cls.args);
+    V3 n = cls.obj->normalAt(cls.hitLoc, cls.args);  // rayHit.obj: the primitive, also through an instance
     n = xvec(nc->adj, n);
     normalize_ip(n);
     cls.objNorm = n;
@@ -625,6 +627,27 @@ struct BVH : AccelStruct {  // :309-423
     if (h2.isHit && (!h.isHit || (h2.t < h.t))) h2 = right->traverse(ray, tr, ctara, st);
     return h.t <= h2.t ? h : h2;
   }
+};
+
+// myInstance (mySceneObject.java:95-145): the named object tested with the instance's
+// transformed ray as both of its rays (so an instanced accel re-normalises that ray in
+// place and tests its boxes with it) and the instance CTM array; the instance shader
+// (`instance <name> shdr`) replaces the hit's. Hits keep the primitive as rayHit.obj.
+struct Instance : GeomBase {
+  GeomBase* obj = nullptr;
+  bool useShader = false;
+  Hit intersect(Ray&, Ray& tr, const CTM* ctara, uint64_t* st) override {
+    Hit h = obj->intersect(tr, tr, ctara, st);
+    if (useShader) h.shdr = shdr;
+    return h;
+  }
+  int shadowHit(Ray&, Ray& tr, const CTM* ctara, double d, uint64_t* st) override {
+    return obj->shadowHit(tr, tr, ctara, d, st);
+  }
+  V3 normalAt(const V3& p, const int* a) override { return obj->normalAt(p, a); }
+  V3 getOrigin(double t) override { return xpt(obj->ctm->g, obj->getOrigin(t)); }
+  V3 getMaxVec() override { return xpt(obj->ctm->g, obj->getMaxVec()); }
+  V3 getMinVec() override { return xpt(obj->ctm->g, obj->getMinVec()); }
 };
 
 // ---------------------------------------------------------------------------
@@ -1574,6 +1597,7 @@ struct Loader {
   double avgNumPerCell = 1.0, mortarThresh = 0.05;
   bool inTmpList = false;
   std::vector<GeomBase*> tmpList;
+  std::map<std::string, GeomBase*> named;  // namedObjs (myScene.java:378-387)
   int curNumRaysPerPxl = 0;
   std::string err;
 
@@ -1693,6 +1717,100 @@ struct Loader {
     }
   }
   double num(const std::vector<std::string>& t, size_t i) { return std::stod(t.at(i)); }
+  // gtTranslate / gtScale / gtRotate (myScene.java:1256-1318)
+  void translate(double x, double y, double z) {
+    M4 T; T.m[0][3] = x; T.m[1][3] = y; T.m[2][3] = z;
+    stack.back() = mmul(stack.back(), T);
+  }
+  void scale(double x, double y, double z) {
+    M4 S; S.m[0][0] = x; S.m[1][1] = y; S.m[2][2] = z;
+    stack.back() = mmul(stack.back(), S);
+  }
+  void rotate(double ang, double ax, double ay, double az) {
+    double ar = (double)(ang * M_PI) / 180.0;
+    V3 av = normalized(V3(ax, ay, az));
+    V3 nv = (ax == 0) ? V3(1, 0, 0) : V3(0, 1, 0);
+    V3 bv = normalized(cross(av, nv));
+    V3 cv = normalized(cross(av, bv));
+    M4 R1, R2;
+    R1.m[0][0] = av.x; R1.m[0][1] = av.y; R1.m[0][2] = av.z;
+    R1.m[1][0] = bv.x; R1.m[1][1] = bv.y; R1.m[1][2] = bv.z;
+    R1.m[2][0] = cv.x; R1.m[2][1] = cv.y; R1.m[2][2] = cv.z;
+    M4 R1T = transpose(R1);
+    R2.m[1][1] = std::cos(ar); R2.m[1][2] = -std::sin(ar); R2.m[2][1] = std::sin(ar); R2.m[2][2] = std::cos(ar);
+    M4 tmp = mmul(R2, R1);
+    stack.back() = mmul(stack.back(), mmul(R1T, tmp));
+  }
+  void push() { stack.push_back(stack.back()); }
+  void pop() { if (stack.size() > 1) stack.pop_back(); }
+  // addInstance (myScene.java:389-395) + myInstance ctor (mySceneObject.java:98-110)
+  bool add_instance(const std::string& name, bool addShdr) {
+    auto it = named.find(name);
+    if (it == named.end()) { err = "unknown named object: " + name; return false; }
+    Instance* in = s->make<Instance>();
+    in->obj = it->second;
+    // myGeomBase ctor: origin (0,0,0) through the stack top; then CTMara = buildCTMara(scene,
+    // obj.glbl) = obj.glbl x stack top (DistRayTracer.java:401)
+    in->trans_origin = xpt(stack.back(), V3(0, 0, 0));
+    in->ctm = std::make_shared<CTM>(build_ctm(mmul(in->obj->ctm->g, stack.back())));
+    in->minVals = in->getMinVec();
+    in->maxVals = in->getMaxVec();
+    make_bbox(s, in);
+    in->key = in->obj->key;  // RNG prim key: the named object's (instances are not primitives)
+    if (addShdr) { in->useShader = true; in->shdr = cur_shader(); }
+    add_object(in);
+    return true;
+  }
+  // setSierpShdr (myScene.java:328-337), float arithmetic as in the reference
+  void sierp_shader(int level, int maxLevel) {
+    float bVal = 1.0f - std::min(1.0f, (1.5f * level / maxLevel)), rVal = 1.0f - bVal,
+          tmp = std::min((1.2f * (level - (maxLevel / 2))) / (1.0f * maxLevel), 1.0f), gVal = (tmp * tmp);
+    Color cd(std::min(1.0f, rVal + .5f), std::min(1.0f, gVal + .5f), std::min(1.0f, bVal + .5f));
+    txTop = false; txBtm = false;
+    set_surface(cd, Color(0, 0, 0), Color(0, 0, 0), 0, 0);
+  }
+  void sierp_shift(float newTrans) { rotate(120, 1, 0, 0); translate(0, newTrans, 0); rotate(-120, 1, 0, 0); }
+  // buildSierpSubTri (myScene.java:339-380)
+  bool sierp_sub(float dim, float scVal, const std::string& name, int level, int maxLevel, bool addShader) {
+    if (level >= maxLevel) return true;
+    float newDim = scVal * dim;
+    push();
+    translate(0, .1f * dim, 0);
+    rotate(70, 0, 1, 0);
+    if (addShader) sierp_shader(level, maxLevel);
+    if (!add_instance(name, addShader)) return false;
+    pop();
+    const float sqrt66 = (float)std::sqrt(6.0f) / 6.0f;  // DistRayTracer.java:38
+    float newTrans = sqrt66 * dim;
+    for (int k = 0; k < 4; ++k) {  // up, front, left, right
+      push();
+      if (k == 0) translate(0, newTrans, 0);
+      else if (k == 1) sierp_shift(newTrans);
+      else if (k == 2) { rotate(120, 0, 1, 0); sierp_shift(newTrans); rotate(-120, 0, 1, 0); }
+      else { rotate(-120, 0, 1, 0); sierp_shift(newTrans); rotate(120, 0, 1, 0); }
+      scale(scVal, scVal, scVal);
+      if (!sierp_sub(newDim, scVal, name, level + 1, maxLevel, addShader)) return false;
+      pop();
+    }
+    return true;
+  }
+  void end_tmp_list(bool bvh) {  // endTmpObjList (myScene.java:305-324)
+    inTmpList = false;
+    if (!bvh) {
+      GeomList* gl = s->make<GeomList>();
+      gl->ctm = cur_ctm();
+      make_bbox(s, gl);
+      for (GeomBase* o : tmpList) gl->add_obj(o);
+      add_object(gl);
+    } else {
+      BVH* root = new_bvh(s, cur_ctm());
+      OList l[3];
+      build_sorted(tmpList, -1, l);
+      add_obj_list(s, root, l, 0, (int)l[0].size() - 1);
+      add_object(root);
+    }
+    tmpList.clear();
+  }
 
   bool read_file(const std::string& fname, bool isMain) {
     std::ifstream f(dir + "/" + fname);
@@ -1825,22 +1943,30 @@ struct Loader {
         } else if (c == "depth") {
         } else if (c == "begin_list") {
           inTmpList = true; tmpList.clear();
-        } else if (c == "end_list" || c == "end_accel") {  // endTmpObjList (myScene.java:305-324)
-          inTmpList = false;
-          if (c == "end_list") {
-            GeomList* gl = s->make<GeomList>();
-            gl->ctm = cur_ctm();
-            make_bbox(s, gl);
-            for (GeomBase* o : tmpList) gl->add_obj(o);
-            add_object(gl);
-          } else {
-            BVH* root = new_bvh(s, cur_ctm());
-            OList l[3];
-            build_sorted(tmpList, -1, l);
-            add_obj_list(s, root, l, 0, (int)l[0].size() - 1);
-            add_object(root);
+        } else if (c == "end_list" || c == "end_accel") {
+          end_tmp_list(c == "end_accel");
+        } else if (c == "named_object") {  // setObjectAsNamedObject (myScene.java:378-387)
+          if (inTmpList || s->objList.empty()) { err = "named_object: no scene object to name"; return false; }
+          GeomBase* o = s->objList.back();
+          s->objList.pop_back();
+          named[t.at(1)] = o;
+        } else if (c == "instance") {  // myRTFileReader.java:250-256: any 3rd token selects the current shader
+          if (!add_instance(t.at(1), t.size() > 2)) return false;
+        } else if (c == "sierpinski") {  // myRTFileReader.java:234-241, buildSierpinski (myScene.java:371-377)
+          std::string objName = t.at(1);
+          float sc = .5f;
+          int depth = 5;
+          bool useShdr = false;  // useShdr != "No": true iff a 5th token was parsed
+          try {
+            depth = std::stoi(t.at(2));
+            sc = std::stof(t.at(3));
+            useShdr = t.size() > 4;
+          } catch (...) {
           }
-          tmpList.clear();
+          if (inTmpList) { err = "sierpinski inside begin_list"; return false; }
+          inTmpList = true; tmpList.clear();
+          if (!sierp_sub(8, sc, objName, 0, depth, useShdr)) return false;
+          end_tmp_list(true);
         } else if (c == "texture" || c == "image_texture") {
           std::string side = t.at(1), lo = side;
           for (auto& ch : lo) ch = (char)tolower(ch);
@@ -2022,34 +2148,19 @@ struct Loader {
           pl->key = s->primCount++;
           add_object(pl);
         } else if (c == "push") {
-          stack.push_back(stack.back());
+          push();
         } else if (c == "pop") {
-          if (stack.size() > 1) stack.pop_back();
+          pop();
         } else if (c == "translate") {
-          M4 T; T.m[0][3] = num(t, 1); T.m[1][3] = num(t, 2); T.m[2][3] = num(t, 3);
-          stack.back() = mmul(stack.back(), T);
+          translate(num(t, 1), num(t, 2), num(t, 3));
         } else if (c == "scale") {
-          M4 S; S.m[0][0] = num(t, 1); S.m[1][1] = num(t, 2); S.m[2][2] = num(t, 3);
-          stack.back() = mmul(stack.back(), S);
-        } else if (c == "rotate") {  // gtRotate (myScene.java:1280-1318)
-          double ang = num(t, 1), ax = num(t, 2), ay = num(t, 3), az = num(t, 4);
-          double ar = (double)(ang * M_PI) / 180.0;
-          V3 av = normalized(V3(ax, ay, az));
-          V3 nv = (ax == 0) ? V3(1, 0, 0) : V3(0, 1, 0);
-          V3 bv = normalized(cross(av, nv));
-          V3 cv = normalized(cross(av, bv));
-          M4 R1, R2;
-          R1.m[0][0] = av.x; R1.m[0][1] = av.y; R1.m[0][2] = av.z;
-          R1.m[1][0] = bv.x; R1.m[1][1] = bv.y; R1.m[1][2] = bv.z;
-          R1.m[2][0] = cv.x; R1.m[2][1] = cv.y; R1.m[2][2] = cv.z;
-          M4 R1T = transpose(R1);
-          R2.m[1][1] = std::cos(ar); R2.m[1][2] = -std::sin(ar); R2.m[2][1] = std::sin(ar); R2.m[2][2] = std::cos(ar);
-          M4 tmp = mmul(R2, R1);
-          stack.back() = mmul(stack.back(), mmul(R1T, tmp));
+          scale(num(t, 1), num(t, 2), num(t, 3));
+        } else if (c == "rotate") {
+          rotate(num(t, 1), num(t, 2), num(t, 3), num(t, 4));
         } else if (c == "reset_timer" || c == "print_timer" || c == "refine") {
           // timers and the progressive `refine` preview are ignored (documented override)
         } else {
-          // other commands (instances, sierpinski, ...) are outside the hot-path scope
+          // remaining commands are outside the hot-path scope
           err = "unsupported command: " + c;
           return false;
         }

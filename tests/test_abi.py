@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(rt.EXPORTS)
-    assert L.rt_abi_version() == 2
+    assert L.rt_abi_version() == 3
 
 
 def test_no_gpu_fails_loudly():
@@ -52,6 +52,11 @@ def test_error_codes():
         rt.inspect_cli("plnts3ColsBunnies.cli", textures={})  # texture not registered
 
 
+# named_object / instance (p3_t01-03, p3_t10-11, p4_t02, p4_t05Alt) and sierpinski layouts
+INSTANCE_SCENES = ["p3_t01.cli", "p3_t02.cli", "p3_t03.cli", "p3_t10.cli", "p3_t11.cli", "p4_t02.cli",
+                   "p4_t05Alt.cli", "p3_t02_sierp.cli", "p3_t11_sierp.cli"]
+
+
 @pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4", "C5"])
 def test_host_builder_matches_oracle_topology(cfg):
     cli = scenes.CONFIGS[cfg][0]
@@ -65,7 +70,7 @@ def test_host_builder_matches_oracle_topology(cfg):
 @pytest.mark.parametrize("cli", ["p2_t03.cli", "p2_t05.cli", "p2_t07.cli", "c2clear.cli", "t05.cli", "p3_t05.cli",
                                  "earth.cli", "cylinder1.cli", "old_t07.cli", "old_t10.cli", "planets3Ortho.cli",
                                  "p3_t09.cli", "p4_t05.cli", "p4_t06_2.cli"] +
-                                [f"p4_st0{i}.cli" for i in range(1, 10)])
+                                [f"p4_st0{i}.cli" for i in range(1, 10)] + INSTANCE_SCENES)
 def test_host_builder_feature_scenes(cli):
     scenes.ensure_bun69k()
     tex = scenes.prepare(cli)

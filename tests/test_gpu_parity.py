@@ -91,6 +91,20 @@ def test_stone_parity(cli):
     assert c["mismatch_frac"] < 2e-3, c
 
 
+@pytest.mark.parametrize("cli,spp", [("p3_t01.cli", 1), ("p3_t02.cli", 2), ("p3_t03.cli", 1), ("p4_t02.cli", 1),
+                                     ("p4_t05Alt.cli", 1), ("p3_t10.cli", 1), ("p3_t11.cli", 2),
+                                     ("p3_t02_sierp.cli", 1), ("p3_t11_sierp.cli", 1)])
+def test_instance_parity(cli, spp):
+    """named_object / instance (myInstance, mySceneObject.java:95-145): instanced spheres
+    (p3_t01-03, scaled), textured (p4_t02, p4_t05Alt), instanced bun69k BVHs with instance
+    shaders (p3_t10, p3_t11: hits stay in the named BVH's space, Q4), and sierpinski BVHs of
+    instances (p3_t02_sierp: 341 spheres; p3_t11_sierp: 21,845 bun69k instances, two-level)."""
+    scenes.ensure_bun69k()
+    g, o, (rg, ag), (ro, ao) = both(cli, 96, 96, spp)
+    c = compare(rg, ag, ro, ao)
+    assert c["mismatch_frac"] < 2e-3, c
+
+
 def test_c3_full_size_properties():
     """BASELINE C3 size (1024^2, 16 spp): deterministic, band-decomposable, and
     matching the oracle on a row subsample."""
@@ -150,7 +164,7 @@ def test_photon_map_parity(tmp_path, mode, spec):
 
 @pytest.mark.parametrize("cli,W,spp", [("c3_bun69k.cli", 128, 2), ("t01.cli", 128, 1), ("p2_t05.cli", 96, 2),
                                        ("c2clear.cli", 96, 1), ("plnts3ColsBunnies.cli", 96, 1),
-                                       ("t11.cli", 64, 1)])
+                                       ("t11.cli", 64, 1), ("p3_t11_sierp.cli", 64, 1)])
 def test_specialised_kernel_equals_generic(cli, W, spp):
     """The feature-specialised kernel variant picked for a scene renders bit-identically
     to the all-features kernel (RT_RENDER_GENERIC)."""
