@@ -42,9 +42,14 @@ def test_error_codes():
     assert L.rt_scene_inspect_cli(str(scenes.SCENE_DIR).encode(), b"does_not_exist.cli", 0, None, None,
                                   info.ctypes.data, 12) == -3  # RT_E_IO
     d = Path(tempfile.mkdtemp())
-    (d / "bad.cli").write_text("fov 60\nnamed_object foo\n")
+    (d / "bad.cli").write_text("fov 60\nfinal_frobnicate foo\n")
     assert L.rt_scene_inspect_cli(str(d).encode(), b"bad.cli", 0, None, None, info.ctypes.data, 12) == -2
     assert b"unsupported command" in L.rt_last_error()
+    (d / "bad3.cli").write_text("fov 60\nnamed_object foo\n")  # nothing to name
+    assert L.rt_scene_inspect_cli(str(d).encode(), b"bad3.cli", 0, None, None, info.ctypes.data, 12) == -2
+    (d / "bad4.cli").write_text("fov 60\ninstance nosuch\n")
+    assert L.rt_scene_inspect_cli(str(d).encode(), b"bad4.cli", 0, None, None, info.ctypes.data, 12) == -2
+    assert b"unknown named object" in L.rt_last_error()
     (d / "bad2.cli").write_text("fov 60\nsphere 1 0 0\n")
     assert L.rt_scene_inspect_cli(str(d).encode(), b"bad2.cli", 0, None, None, info.ctypes.data, 12) == -2
     assert L.rt_scene_inspect_cli(None, b"x.cli", 0, None, None, info.ctypes.data, 12) == -1
