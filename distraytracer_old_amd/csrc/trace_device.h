@@ -300,8 +300,8 @@ DEVI bool planar_test(const double (*v)[3], V nA, V nB, double dA, double dB, V 
   return true;
 }
 
-template <class LIM = LimNone>
-DEVI bool tri_test(const TriD& T, V o, V d, double& t, int& st, const LIM& lim = LIM()) {
+template <class LIM = LimNone, class TR = TriD>  // TR: TriD or its geometry part (TriG)
+DEVI bool tri_test(const TR& T, V o, V d, double& t, int& st, const LIM& lim = LIM()) {
   V nA = ld3(T.n);
   V nB = mk(-nA.x, -nA.y, -nA.z);  // exactly the reversed-order normal
   return planar_test<3, false>(T.v, nA, nB, T.dA, T.dB, o, d, t, st, lim);

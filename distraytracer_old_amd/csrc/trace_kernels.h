@@ -66,6 +66,74 @@ DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, double&
 }
 template <uint32_t F>
 DEVI int32_t ref_xf(const SceneD& S, int32_t ref) { return (!(F & FT_PRIM) || ref >= 0) ? S.tri[ref].xf : S.prim[~ref].xf; }
+
+// Scalar (SMEM) loads of scene records at wave-uniform addresses: through the constant
+// address space a uniform load is selected as s_load into SGPRs (the packet traversal
+// below, where every lane of a wave works on the same node / triangle).
+// (Field by field: an aggregate copy through the cast is turned back into global loads.)
+template <class T>
+DEVI T sload(const T* p) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "scalar field");
+  return *(const __attribute__((address_space(4))) T*)p;
+}
+struct ChildBox {  // one child of a NodeD: box + reference
+  double mn[3], mx[3];
+  int32_t ref;
+};
+DEVI ChildBox sload_child(const NodeD* nd, int side) {
+  ChildBox c;
+  const double* b = side ? nd->rmin : nd->lmin;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { c.mn[i] = sload(b + i); c.mx[i] = sload(b + 3 + i); }
+  c.ref = sload(side ? &nd->right : &nd->left);
+  return c;
+}
+struct TriG {  // the part of a TriD the triangle test reads
+  double v[3][3];
+  double n[3];
+  double dA, dB;
+};
+DEVI TriG sload_tri(const TriD* t) {
+  TriG g;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) g.v[i][c] = sload(&t->v[i][c]);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) g.n[c] = sload(&t->n[c]);
+  g.dA = sload(&t->dA);
+  g.dB = sload(&t->dB);
+  return g;
+}
+DEVI TopD sload_top(const TopD* p) {
+  TopD t;
+  t.kind = sload(&p->kind); t.idx = sload(&p->idx); t.xf = sload(&p->xf); t.key = sload(&p->key);
+  return t;
+}
+DEVI int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+DEVI uint64_t uni64(uint64_t v) {
+  return ((uint64_t)(uint32_t)uni((int32_t)(v >> 32)) << 32) | (uint32_t)uni((int32_t)(uint32_t)v);
+}
+DEVI bool in_mask(uint64_t m) { return (m >> __lane_id()) & 1; }
+
+// a primitive test whose triangle record is loaded at a wave-uniform address (PK)
+template <bool CNT, uint32_t F, bool PK, class LIM = LimNone>
+DEVI bool test_ref_u(const SceneD& S, int32_t ref, V o, V d, const Key& k, double& t, int& args, Counters& ct,
+                     const LIM& lim = LIM()) {
+  if constexpr (PK) {
+    if (!(F & FT_PRIM) || ref >= 0) {
+      if (CNT) ct.c[C_TRI]++;
+      const TriG T = sload_tri(S.tri + ref);
+      return tri_test(T, o, d, t, args, lim);
+    }
+  }
+  return test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, lim);
+}
+template <uint32_t F, bool PK>
+DEVI int32_t ref_xf_u(const SceneD& S, int32_t ref) {
+  if (PK && (!(F & FT_PRIM) || ref >= 0)) return sload(&S.tri[ref].xf);
+  return ref_xf<F>(S, ref);
+}
 template <uint32_t F>
 DEVI bool is_inst(const SceneD& S, int32_t ref) { return (F & FT_INST) && ref < 0 && S.prim[~ref].type == PT_INST; }
 
@@ -80,14 +148,19 @@ struct LeafR {
   int32_t start, count;
   bool run;
 };
+template <bool PK = false>
 DEVI LeafR leaf_of(const SceneD& S, int32_t c) {
   LeafR r;
   r.run = (c & LEAF_RUN_FLAG) != 0;
   if (r.run) { r.start = (c >> 5) & LEAF_RUN_MAXSTART; r.count = c & 31; }
+  else if (PK) { r.start = sload(&S.leaf[c].start); r.count = sload(&S.leaf[c].count); }
   else { LeafD lf = S.leaf[c]; r.start = lf.start; r.count = lf.count; }
   return r;
 }
-DEVI int32_t leaf_member(const SceneD& S, const LeafR& lf, int i) { return lf.run ? lf.start + i : S.member[lf.start + i]; }
+template <bool PK = false>
+DEVI int32_t leaf_member(const SceneD& S, const LeafR& lf, int i) {
+  return lf.run ? lf.start + i : (PK ? sload(S.member + lf.start + i) : S.member[lf.start + i]);
+}
 
 template <bool CNT, uint32_t F>
 DEVI void inst_closest(const SceneD& S, int32_t ii, WRay& w, const Key& k, int top, Best& best, double& local, Counters& ct);
@@ -95,13 +168,14 @@ DEVI void inst_closest(const SceneD& S, int32_t ii, WRay& w, const Key& k, int t
 // myGeomList.traverseStruct leaf loop (myGeomBase.java:281-296): strict <, leaf order.
 // w is the leaf's `_ray`: the world ray, or (INST) the instance ray of an instanced accel;
 // accXf >= 0: members with that CTM reuse the accel-space ray (ao, ad) while w is unchanged.
-template <bool CNT, uint32_t F, bool INST>
+// PK: `leaf` is wave-uniform (packet traversal): member records are loaded as scalars.
+template <bool CNT, uint32_t F, bool INST, bool PK = false>
 DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w, const Key& k, const HitCtx& hc,
                        Best& best, double& local, Counters& ct) {
-  const LeafR lf = leaf_of(S, leaf);
+  const LeafR lf = leaf_of<PK>(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
   for (int i = 0; i < lf.count; ++i) {
-    int32_t ref = leaf_member(S, lf, i);
+    int32_t ref = leaf_member<PK>(S, lf, i);
     renorm(w);  // _ray.getTransformedRay(_ray, obj.CTMara[invIDX])
     if constexpr (!INST && (F & FT_INST) != 0) {
       if (is_inst<F>(S, ref)) {  // a sierpinski element: myInstance.intersectCheck
@@ -109,13 +183,13 @@ DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRa
         continue;
       }
     }
-    int xf = ref_xf<F>(S, ref);
+    int xf = ref_xf_u<F, PK>(S, ref);
     V o, d;
     if (xf == accXf && !w.moved) { o = ao; d = ad; }
     else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
     double t;
     int args;
-    if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, LimClosest{local, best.t})) {
+    if (test_ref_u<CNT, F, PK>(S, ref, o, d, k, t, args, ct, LimClosest{local, best.t})) {
       if (t < local) local = t;
       if (t < best.t) {
         best.t = t; best.ref = ref; best.top = (int16_t)hc.top; best.inAcc = 1; best.inst = hc.inst;
@@ -141,7 +215,15 @@ static constexpr int STK_LDS = RT_STACK_LDS;
 // per-round sample colours (used only between traversals)
 extern __shared__ double rt_lds[];
 static constexpr int LDS_STACK_BYTES = STK_LDS * 64 * 12;
-static constexpr int LDS_BYTES = LDS_STACK_BYTES > 64 * 4 * 8 ? LDS_STACK_BYTES : 64 * 4 * 8;
+// Packet traversal (below): per-lane subtree minima for the first PK_LDS levels
+// ([level][lane] doubles), then the wave-uniform frames: lane masks and node<<1|phase.
+#ifndef RT_PK_LDS
+#define RT_PK_LDS 16
+#endif
+static constexpr int PK_LDS = RT_PK_LDS;
+static constexpr int LDS_PK_BYTES = PK_LDS * 64 * 8 + BVH_STACK * 8 + BVH_STACK * 4;
+static constexpr int LDS_MAX2 = LDS_STACK_BYTES > LDS_PK_BYTES ? LDS_STACK_BYTES : LDS_PK_BYTES;
+static constexpr int LDS_BYTES = LDS_MAX2 > 64 * 4 * 8 ? LDS_MAX2 : 64 * 4 * 8;
 typedef __attribute__((address_space(3))) double lds_f64;
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 DEVI lds_f64* ldsT() { return (lds_f64*)rt_lds; }
@@ -235,6 +317,91 @@ DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, RayInv ri,
   if (local < outer) outer = local;
 }
 
+// ---------------------------------------------------------------------------
+// Packet traversal. The lanes of a wave trace nearly the same rays (the samples of a
+// 2x2 pixel tile), so the wave walks ONE node sequence -- the union of its lanes' --
+// with wave-uniform control: node indices, frames and lane masks live in SGPRs / LDS,
+// node and triangle records are scalar loads (s_load into SGPRs), and a lane executes
+// the box and leaf tests only at the nodes its own sequential traversal visits (lane
+// mask per frame). Each lane therefore performs exactly the tests of accel_closest /
+// accel_any above, in the same order, with the same pruning -- the results (and the
+// instrumented counters) are identical; only idle lanes wait.
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+DEVI lds_f64* pkT() { return (lds_f64*)rt_lds; }
+DEVI lds_u64* pkM() { return (lds_u64*)(rt_lds + PK_LDS * 64); }
+DEVI lds_i32* pkN() { return (lds_i32*)(rt_lds + PK_LDS * 64 + BVH_STACK); }
+struct PkStack {
+  double sT[BVH_STACK - PK_LDS];  // per-lane subtree minima below the LDS levels
+  DEVI double getT(int i) const { return i < PK_LDS ? pkT()[i * 64 + __lane_id()] : sT[i - PK_LDS]; }
+  DEVI void setT(int i, double v) {
+    if (i < PK_LDS) pkT()[i * 64 + __lane_id()] = v;
+    else sT[i - PK_LDS] = v;
+  }
+  // wave-uniform frame: every active lane writes the same value; read back as a scalar
+  DEVI void setFrame(int i, int32_t n, uint64_t m) { pkN()[i] = n; pkM()[i] = m; }
+  DEVI void setN(int i, int32_t n) { pkN()[i] = n; }
+  DEVI int32_t getN(int i) const { return uni(pkN()[i]); }
+  DEVI uint64_t getM(int i) const { return uni64(pkM()[i]); }
+};
+
+// accel_closest<INST = false> as a packet traversal (same per-lane semantics)
+template <bool CNT, uint32_t F>
+DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv ri, WRay& w, const Key& k,
+                           const HitCtx& hc, Best& best, double& outer, Counters& ct) {
+  PkStack st;
+  int sp = 0;
+  double local = DMAX;
+  uint64_t act = __ballot(1);  // lanes in the current subtree
+  int32_t N = uni(A.root);
+  const int32_t axf = A.xf;
+  while (true) {
+    // descend: push N, go left with the lanes whose left box is hit
+    while (N >= 0) {
+      const ChildBox cl = sload_child(S.node + N, 0);
+      st.setFrame(sp, N << 1, act);
+      bool hl = false;
+      if (in_mask(act)) {
+        if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }
+        st.setT(sp, local);
+        local = DMAX;
+        hl = box_hit(cl.mn, cl.mx, ao, ad, ri);
+      }
+      sp++;
+      const uint64_t H = __ballot(hl);
+      if (H) { act = H; N = cl.ref; }
+      else { N = INT32_MAX; break; }
+    }
+    if (N != INT32_MAX && in_mask(act)) leaf_closest<CNT, F, false, true>(S, ~N, axf, ao, ad, w, k, hc, best, local, ct);
+    // unwind
+    N = INT32_MAX;
+    while (sp > 0) {
+      const int32_t np = st.getN(sp - 1);
+      const uint64_t M = st.getM(sp - 1);
+      if ((np & 1) == 0) {
+        const ChildBox cr = sload_child(S.node + (np >> 1), 1);
+        bool gr = false;
+        if (in_mask(M)) gr = box_before(cr.mn, cr.mx, ao, ad, ri, local);
+        const uint64_t R = __ballot(gr);
+        if (R) {
+          st.setN(sp - 1, np | 1);
+          act = R;
+          N = cr.ref;
+          break;
+        }
+      }
+      // this node's minimal t joins the enclosing subtree's
+      if (in_mask(M)) {
+        const double sv = st.getT(sp - 1);
+        if (sv < local) local = sv;
+      }
+      act = M;
+      sp--;
+    }
+    if (N == INT32_MAX) break;
+  }
+  if (local < outer) outer = local;
+}
+
 // myInstance.intersectCheck (mySceneObject.java:119-124): the named object tested with
 // the instance ray (instance CTM inverse x w) as both of its rays; for a named accel
 // that ray is re-normalised in place by its leaves. `local` receives the minimal t.
@@ -272,11 +439,16 @@ DEVI void inst_closest(const SceneD& S, int32_t ii, WRay& w, const Key& k, int t
 }
 
 // findClosestRayHit (myScene.java:888-903): objList scan, TreeMap keeps the first of equal t
-template <bool CNT, uint32_t F>
+#ifndef RT_PACKET
+#define RT_PACKET 1
+#endif
+static constexpr bool PACKET = RT_PACKET != 0;  // render kernel: packet traversal
+// PK: packet traversal of the BVHs (render kernel; the lanes of a wave are coherent)
+template <bool CNT, uint32_t F, bool PK = false>
 DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
   Best best = miss();
   for (int i = 0; i < S.ntop; ++i) {
-    TopD tp = S.top[i];
+    TopD tp = PK ? sload_top(S.top + i) : S.top[i];
     if (CNT) ct.c[C_TOP]++;
     renorm(w);
     if ((F & FT_INST) && tp.kind == TOP_INST) {
@@ -293,7 +465,8 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       if (!box_hit(A.bmin, A.bmax, o, d, ri)) continue;
       w.moved = false;
       double local = DMAX;
-      accel_closest<CNT, F, false>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
+      if (PK) accel_closest_pk<CNT, F>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
+      else accel_closest<CNT, F, false>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
     } else {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
@@ -316,12 +489,12 @@ DEVI bool shadow_box(const double* mn, const double* mx, V o, V d, const RayInv&
 template <bool CNT, uint32_t F>
 DEVI bool inst_any(const SceneD& S, int32_t ii, const WRay& w, const Key& k, double dist, Counters& ct);
 
-template <bool CNT, uint32_t F, bool INST>
+template <bool CNT, uint32_t F, bool INST, bool PK = false>
 DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
-  const LeafR lf = leaf_of(S, leaf);
+  const LeafR lf = leaf_of<PK>(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
   for (int i = 0; i < lf.count; ++i) {
-    int32_t ref = leaf_member(S, lf, i);
+    int32_t ref = leaf_member<PK>(S, lf, i);
     renorm(w);
     if constexpr (!INST && (F & FT_INST) != 0) {
       if (is_inst<F>(S, ref)) {  // myInstance.calcShadowHit
@@ -329,13 +502,13 @@ DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w
         continue;
       }
     }
-    int xf = ref_xf<F>(S, ref);
+    int xf = ref_xf_u<F, PK>(S, ref);
     V o, d;
     if (xf == accXf && !w.moved) { o = ao; d = ad; }
     else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
     double t;
     int args;
-    if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, LimShadow{dist}) && (dist - t) > EPS) return true;
+    if (test_ref_u<CNT, F, PK>(S, ref, o, d, k, t, args, ct, LimShadow{dist}) && (dist - t) > EPS) return true;
   }
   return false;
 }
@@ -365,6 +538,58 @@ DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const
     if (N == INT32_MAX) return false;
   }
 }
+// accel_any<INST = false> as a packet traversal; a lane leaves the packet when blocked
+template <bool CNT, uint32_t F>
+DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
+  const RayInv ri = ray_inv(ao, ad, S.fastSlab);
+  PkStack st;
+  int sp = 0;
+  uint64_t act = __ballot(1);
+  uint64_t alive = act;
+  bool blocked = false;
+  int32_t N = uni(A.root);
+  const int32_t axf = A.xf;
+  // leafVals.calcShadowHit tests its own box first; myBVH.calcShadowHit (internal) does not
+  if (N < 0) {
+    bool hb = false;
+    if (in_mask(act)) hb = shadow_box<CNT>(A.bmin, A.bmax, ao, ad, ri, dist, ct);
+    act = __ballot(hb);
+    if (!act) return false;
+  }
+  while (true) {
+    if (N >= 0) {  // internal: push (right child pending), go left with the lanes whose left box is hit
+      const ChildBox cl = sload_child(S.node + N, 0);
+      st.setFrame(sp, N, act);
+      sp++;
+      bool hl = false;
+      if (in_mask(act)) {
+        if (CNT) ct.c[C_NODE]++;
+        hl = shadow_box<CNT>(cl.mn, cl.mx, ao, ad, ri, dist, ct);
+      }
+      const uint64_t H = __ballot(hl);
+      if (H) { act = H; N = cl.ref; continue; }
+    } else if (N != INT32_MAX) {
+      bool b = false;
+      if (in_mask(act)) b = leaf_any<CNT, F, false, true>(S, ~N, axf, ao, ad, w, k, dist, ct);
+      if (b) blocked = true;
+      alive &= ~__ballot(b);
+      if (!alive) return blocked;
+    }
+    N = INT32_MAX;
+    while (sp > 0) {
+      --sp;
+      const uint64_t M = st.getM(sp) & alive;
+      if (!M) continue;
+      const ChildBox cr = sload_child(S.node + st.getN(sp), 1);
+      bool hr = false;
+      if (in_mask(M)) hr = shadow_box<CNT>(cr.mn, cr.mx, ao, ad, ri, dist, ct);
+      const uint64_t R = __ballot(hr);
+      if (R) { act = R; N = cr.ref; break; }
+    }
+    if (N == INT32_MAX) return blocked;
+  }
+}
+
 // myInstance.calcShadowHit (mySceneObject.java:115-118): obj.calcShadowHit(_trans, _trans, ...)
 template <bool CNT, uint32_t F>
 DEVI bool inst_any(const SceneD& S, int32_t ii, const WRay& w, const Key& k, double dist, Counters& ct) {
@@ -384,10 +609,10 @@ DEVI bool inst_any(const SceneD& S, int32_t ii, const WRay& w, const Key& k, dou
   return false;
 }
 // myScene.calcShadow (myScene.java:879-885)
-template <bool CNT, uint32_t F>
+template <bool CNT, uint32_t F, bool PK = false>
 DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters& ct) {
   for (int i = 0; i < S.ntop; ++i) {
-    TopD tp = S.top[i];
+    TopD tp = PK ? sload_top(S.top + i) : S.top[i];
     if (CNT) ct.c[C_TOP]++;
     renorm(w);
     if ((F & FT_INST) && tp.kind == TOP_INST) {
@@ -399,7 +624,9 @@ DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters
     if (tp.kind == TOP_ACCEL) {
       if (CNT) ct.c[C_ROOT]++;
       w.moved = false;
-      if (accel_any<CNT, F, false>(S, S.accel[tp.idx], o, d, w, k, dist, ct)) return true;
+      if (PK ? accel_any_pk<CNT, F>(S, S.accel[tp.idx], o, d, w, k, dist, ct)
+             : accel_any<CNT, F, false>(S, S.accel[tp.idx], o, d, w, k, dist, ct))
+        return true;
     } else {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
@@ -1127,7 +1354,7 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
 #ifdef RT_PROF_NOSHADOW  // profiling builds only (tools/variant_sweep.py): results differ
     if (false)
 #endif
-    if (shadowed<CNT, F>(S, sr, sk, t, ct)) continue;
+    if (shadowed<CNT, F, PACKET>(S, sr, sk, t, ct)) continue;
     renorm(sr);  // shadowRay.direction._normalize()
     double ldp = dot(sr.d, h.nrm) * ltMult;
     if (ldp > EPS) {
@@ -1345,7 +1572,7 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
       WRay w;
       w.o = in.o; w.d = nrmz(in.d); w.d0 = w.d; w.stable = false; w.moved = false; w.ver = 0;  // myRay ctor
       k.node = in.node;
-      Best b = closest<CNT, F>(S, w, k, ct);
+      Best b = closest<CNT, F, PACKET>(S, w, k, ct);
       if (b.t == DMAX) {
         c = background<CNT, F>(S, w, ct);
       } else {

@@ -27,7 +27,8 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "knnheap": ["RT_KNN_HEAP"],
     "nophong": ["RT_PROF_NOPHONG"],
 }
-FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS", "g": "RT_MAX_G"}
+FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS", "g": "RT_MAX_G", "p": "RT_PACKET",
+          "l": "RT_PK_LDS"}
 
 
 def defines_of(name: str) -> list[str]:
