@@ -168,6 +168,11 @@ def main():
             if rank == 0:
                 full_img[:] = multigpu.assemble(gathered, H)
 
+    # setup (untimed, like the counting run): a layout's first two renders calibrate its tile
+    # dispatch order (probe, then measured wave times; rt_render_device in include/distraytracer.h)
+    for _ in range(2):
+        scene.render_device(p, rgb.data_ptr(), argb.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()

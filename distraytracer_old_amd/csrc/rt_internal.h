@@ -63,6 +63,13 @@ struct rt_scene {
   size_t devBytes = 0;
   bool photonsUploaded = false;
   void* counters = nullptr;  // device uint64[RT_ST_N]
-  // tile schedules (longest tiles first) per tile layout: key -> device int32[tiles]
-  std::vector<std::pair<std::string, int32_t*>> schedules;
+  // tile schedules (longest tiles first) per tile layout (trace.hip `schedule`)
+  struct TileSchedule {
+    std::string key;
+    int32_t* order;  // device int32[ntiles]: dispatch position -> tile
+    uint32_t* cost;  // device uint32[ntiles]: probe cost, then one launch's measured wave times
+    int ntiles;
+    int state;       // 0 probe order; 1 a measuring launch was issued; 2 ordered by measured times
+  };
+  std::vector<TileSchedule> schedules;
 };

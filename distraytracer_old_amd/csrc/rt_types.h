@@ -159,6 +159,7 @@ struct ParamsD {
   // 64/G pixels per wave as a tw x th tile
   int32_t G, tw, th, band;  // band: output row ri is image row row0 + (ri/band)*rowStep*band + ri%band
   const int32_t* order;     // tile dispatch order (longest first), nullptr = row-major
+  uint32_t* tcost;          // non-null: each wave writes its duration (s_memrealtime ticks) to tcost[tile]
   // camera (RT_CAMERA_*) with its per-image constants (setImageSize, myScene.java:780-792)
   int32_t cam, pad2;
   double fishMult, xStart, yStart, aperHalf;  // fisheye

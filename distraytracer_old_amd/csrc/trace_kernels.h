@@ -1644,6 +1644,9 @@ DEVI int tile_of_block(int b, int ntiles) {
 #ifndef RT_RENDER_WAVES
 #define RT_RENDER_WAVES 4
 #endif
+#ifdef RT_PROF_TIMELINE  // profiling builds only (tools/timeline.py): per-workgroup start/end clock + HW ids
+__device__ unsigned long long* rt_tl_buf;
+#endif
 template <bool CNT, uint32_t F>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_RENDER_WAVES)))
 render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict__ argb, unsigned long long* __restrict__ gcount) {
@@ -1660,6 +1663,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   int tile = tile_of_block(blockIdx.x, tilesX * ((P.nrows + P.th - 1) / P.th));
   if (tile < 0) return;  // padding block of the XCD mapping (whole workgroup)
   if (P.order) tile = P.order[tile];
+  const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();  // wave start (tcost / timeline)
   const int tx = tile % tilesX, ty = tile / tilesX;
   const int col = tx * P.tw + pl % P.tw;
   const int ri = ty * P.th + pl / P.tw;  // row index within this render's rows
@@ -1788,6 +1792,16 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
     for (int i = 0; i < C_N; ++i)
       if (ct.c[i]) atomicAdd(&gcount[i], (unsigned long long)ct.c[i]);
   }
+  if (!CNT && P.tcost && lane == 0) P.tcost[tile] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tl0);
+#ifdef RT_PROF_TIMELINE
+  if (!CNT && lane == 0 && rt_tl_buf) {
+    unsigned long long* b = rt_tl_buf + 4 * (size_t)blockIdx.x;
+    b[0] = tl0;
+    b[1] = __builtin_amdgcn_s_memrealtime();
+    b[2] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));  // HW_ID
+    b[3] = ((unsigned)__builtin_amdgcn_s_getreg(20 | (3 << 11))) | ((unsigned long long)tile << 8);  // XCC_ID
+  }
+#endif
 }
 
 // Tile cost probe for the dispatch schedule: one lane per tile traces the tile's first

@@ -225,12 +225,15 @@ int rt_photons_set(rt_scene* scene, const double* pos, const double* pwr, int64_
 /* Blocking render into caller-owned HOST buffers (either may be NULL).
    rgb: float[n_rows*width*3] clamped <=1 per myColor; argb: int32[n_rows*width], reference packing. */
 int rt_render(rt_scene* scene, const rt_render_params* p, float* rgb, int32_t* argb);
-/* Asynchronous render into caller-owned DEVICE buffers on `hip_stream` (hipStream_t, may be NULL). */
+/* Asynchronous render into caller-owned DEVICE buffers on `hip_stream` (hipStream_t, may be NULL).
+   Tile dispatch order (never the pixels): the first render of a row layout orders tiles by a probe
+   and records its waves' durations; the next render of that layout synchronises once and orders the
+   tiles by those measured times (longest first). Render a layout twice before timing it. */
 int rt_render_device(rt_scene* scene, const rt_render_params* p, float* d_rgb, int32_t* d_argb, void* hip_stream);
 /* Instrumented render (per-lane counters, RT_ST_*): same image, slower; stats: uint64[RT_ST_N]. */
 int rt_render_count(rt_scene* scene, const rt_render_params* p, float* rgb, int32_t* argb, uint64_t* stats);
 /* Kernel-only timing helper: average ms of the render kernel over `iters` launches (HIP events on the
-   launch stream), inputs resident in HBM. */
+   launch stream), inputs resident in HBM; at least 2 warmup launches (the schedule calibration). */
 int rt_time_render(rt_scene* scene, const rt_render_params* p, int warmup, int iters, double* avg_ms);
 
 #ifdef __cplusplus
