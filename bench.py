@@ -8,7 +8,7 @@ workload C3 = scenes/c3_bun69k.cli (data/p3_t09.cli without `wood`) with the
 One step = one full C3 frame: every rank renders its rows (rank r renders the
 8-row bands r, r+N, r+2N, ... -- interleaved for load balance) with the HIP kernel into a
 device buffer, then (N>1) the per-rank float-RGB tiles are gathered to rank 0
-over RCCL (`all_gather_into_tensor`). Work per step is one frame whatever N is
+over RCCL (`dist.gather`: one point-to-point send per rank over xGMI). Work per step is one frame whatever N is
 (strong scaling). value = traced rays of the frame (camera + shadow + reflection
 + refraction, counted exactly by an instrumented run before timing) / max-over-
 ranks step time.
@@ -153,7 +153,7 @@ def main():
 
     rgb = torch.empty((maxrows, W, 3), dtype=torch.float32, device="cuda")
     argb = torch.empty((maxrows, W), dtype=torch.int32, device="cuda")
-    gathered = torch.empty((world, maxrows, W, 3), dtype=torch.float32, device="cuda") if dist else None
+    gathered = torch.empty((world, maxrows, W, 3), dtype=torch.float32, device="cuda") if dist and rank == 0 else None
     stream = torch.cuda.current_stream()
     full_img = torch.empty((H, W, 3), dtype=torch.float32, device="cuda") if dist and rank == 0 else None
 
@@ -163,8 +163,8 @@ def main():
         scene.render_device(p, rgb.data_ptr(), argb.data_ptr(), stream.cuda_stream)
         if ev:
             ev[1].record(stream)
-        if dist:  # the single exchange: float-RGB tiles over RCCL, re-interleaved on rank 0
-            dist.all_gather_into_tensor(gathered.view(-1), rgb.view(-1))
+        if dist:  # the single exchange: float-RGB tiles to rank 0 over RCCL, re-interleaved there
+            multigpu.gather_tiles(rgb, dist, out=gathered)
             if rank == 0:
                 full_img[:] = multigpu.assemble(gathered, H)
 
@@ -219,7 +219,7 @@ def main():
             "config": {"workload": workload, "width": W, "height": H, "spp": spp, "seed": seed,
                        "rays_per_frame": int(rays_frame), "camera_samples": int(cam_frame),
                        "parallelism": f"{multigpu.BAND}-row bands interleaved over {world} rank(s)" +
-                                      (" + RCCL all_gather of float RGB tiles" if world > 1 else "")},
+                                      (" + RCCL gather of float RGB tiles to rank 0" if world > 1 else "")},
             "camera_msamples_per_s": cam_frame / (ms_per_step / 1e3) / 1e6,
             "achieved_hbm_gbps": achieved,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",

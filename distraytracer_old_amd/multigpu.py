@@ -4,8 +4,8 @@ Rank r of N renders row bands r, r+N, r+2N, ... of BAND rows each (interleaved
 bands balance the expensive bunny/glass regions; bands keep a wave's 2-row pixel
 tiles on adjacent image rows, which single-row interleaving at large N would not).
 Every rank's tile is padded to the same row count (a multiple of the band) so one
-`all_gather_into_tensor` (RCCL over xGMI; gloo in CPU tests) brings all float-RGB
-tiles to every rank, and `assemble` re-interleaves them.
+`gather` (RCCL point-to-point over xGMI; gloo in CPU tests) brings all float-RGB
+tiles to rank 0, and `assemble` re-interleaves them.
 
 Pixels, their RNG keys and their per-pixel sample order do not depend on N,
 so the assembled image is bit-identical to the 1-GPU image.
@@ -44,14 +44,20 @@ def assemble(gathered, H: int, band: int = BAND):
     return full[:H]
 
 
-def gather_tiles(tile, dist, group=None):
-    """all_gather equal-size padded tiles (tensor [maxrows, W, C]) -> [world, maxrows, W, C]."""
+def gather_tiles(tile, dist, group=None, dst: int = 0, out=None):
+    """The single exchange: gather equal-size padded tiles (tensor [maxrows, W, C]) to rank
+    `dst` -> [world, maxrows, W, C] there, None on the other ranks. Over RCCL this is one
+    point-to-point send per rank into dst (dist.gather = grouped ncclSend/ncclRecv): on
+    fully connected xGMI each rank's tile crosses its own link to dst once, instead of the
+    world-1 ring steps an all-gather pays for copies nobody but dst needs."""
     import torch
 
     world = dist.get_world_size(group)
-    out = torch.empty((world,) + tuple(tile.shape), dtype=tile.dtype, device=tile.device)
-    dist.all_gather_into_tensor(out.view(-1), tile.contiguous().view(-1), group=group)
-    return out
+    rank = dist.get_rank(group)
+    if rank == dst and out is None:
+        out = torch.empty((world,) + tuple(tile.shape), dtype=tile.dtype, device=tile.device)
+    dist.gather(tile.contiguous(), list(out.unbind(0)) if rank == dst else None, dst=dst, group=group)
+    return out if rank == dst else None
 
 
 def photon_shard(rank: int, world: int, count: int) -> tuple[int, int]:

@@ -42,9 +42,10 @@ def _worker(rank, world, port, H, W, q):
     tile = torch.zeros((multigpu.max_tile_rows(world, H, band), W, 3), dtype=torch.float32)
     tile[: rgb.shape[0]] = torch.from_numpy(rgb)
     g = multigpu.gather_tiles(tile, dist)
-    full = multigpu.assemble(g, H, band)
     if rank == 0:
-        q.put(full.numpy())
+        q.put(multigpu.assemble(g, H, band).numpy())
+    else:
+        assert g is None
     dist.barrier()
     dist.destroy_process_group()
 
