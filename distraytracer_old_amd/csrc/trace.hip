@@ -302,9 +302,15 @@ static int sort_tiles(rt_scene::TileSchedule& e, hipStream_t st) {
   hipError_t r = hipStreamSynchronize(st);
   if (r == hipSuccess) r = hipMemcpy(cost.data(), e.cost, sizeof(uint32_t) * e.ntiles, hipMemcpyDeviceToHost);
   if (r != hipSuccess) return set_error(RT_E_HIP, std::string("tile schedule: ") + hipGetErrorString(r));
-  std::vector<int32_t> order(e.ntiles);
-  for (int i = 0; i < e.ntiles; ++i) order[i] = i;
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+  // sort key: cost in quarter-octave buckets; tiles of one bucket keep row-major order, so
+  // waves running at the same time stay spatially close (shared cache lines) while the
+  // order stays longest-first to within 19 %
+  std::vector<int32_t> order(e.ntiles), key(e.ntiles);
+  for (int i = 0; i < e.ntiles; ++i) {
+    order[i] = i;
+    key[i] = cost[i] ? (int32_t)std::floor(4.0 * std::log2((double)cost[i])) : -1;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key[a] > key[b]; });
   HIPCHK(hipMemcpy(e.order, order.data(), sizeof(int32_t) * e.ntiles, hipMemcpyHostToDevice));
   return RT_OK;
 }

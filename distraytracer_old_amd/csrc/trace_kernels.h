@@ -216,12 +216,17 @@ static constexpr int STK_LDS = RT_STACK_LDS;
 extern __shared__ double rt_lds[];
 static constexpr int LDS_STACK_BYTES = STK_LDS * 64 * 12;
 // Packet traversal (below): per-lane subtree minima for the first PK_LDS levels
-// ([level][lane] doubles), then the wave-uniform frames: lane masks and node<<1|phase.
+// ([level][lane] doubles), then the wave-uniform frames: lane masks (subtree; right box
+// hit, shadow rays), node<<1|phase and the right child (shadow rays).
 #ifndef RT_PK_LDS
 #define RT_PK_LDS 16
 #endif
 static constexpr int PK_LDS = RT_PK_LDS;
-static constexpr int LDS_PK_BYTES = PK_LDS * 64 * 8 + BVH_STACK * 8 + BVH_STACK * 4;
+static constexpr int PKO_M = PK_LDS * 64 * 8;  // byte offsets in rt_lds
+static constexpr int PKO_R = PKO_M + BVH_STACK * 8;
+static constexpr int PKO_N = PKO_R + BVH_STACK * 8;
+static constexpr int PKO_C = PKO_N + BVH_STACK * 4;
+static constexpr int LDS_PK_BYTES = PKO_C + BVH_STACK * 4;
 static constexpr int LDS_MAX2 = LDS_STACK_BYTES > LDS_PK_BYTES ? LDS_STACK_BYTES : LDS_PK_BYTES;
 static constexpr int LDS_BYTES = LDS_MAX2 > 64 * 4 * 8 ? LDS_MAX2 : 64 * 4 * 8;
 typedef __attribute__((address_space(3))) double lds_f64;
@@ -327,9 +332,13 @@ DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, RayInv ri,
 // accel_any above, in the same order, with the same pruning -- the results (and the
 // instrumented counters) are identical; only idle lanes wait.
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
+typedef __attribute__((address_space(3))) char lds_u8;
+DEVI lds_u8* pkB() { return (lds_u8*)rt_lds; }
 DEVI lds_f64* pkT() { return (lds_f64*)rt_lds; }
-DEVI lds_u64* pkM() { return (lds_u64*)(rt_lds + PK_LDS * 64); }
-DEVI lds_i32* pkN() { return (lds_i32*)(rt_lds + PK_LDS * 64 + BVH_STACK); }
+DEVI lds_u64* pkM() { return (lds_u64*)(pkB() + PKO_M); }
+DEVI lds_u64* pkR() { return (lds_u64*)(pkB() + PKO_R); }
+DEVI lds_i32* pkN() { return (lds_i32*)(pkB() + PKO_N); }
+DEVI lds_i32* pkC() { return (lds_i32*)(pkB() + PKO_C); }
 struct PkStack {
   double sT[BVH_STACK - PK_LDS];  // per-lane subtree minima below the LDS levels
   DEVI double getT(int i) const { return i < PK_LDS ? pkT()[i * 64 + __lane_id()] : sT[i - PK_LDS]; }
@@ -342,6 +351,12 @@ struct PkStack {
   DEVI void setN(int i, int32_t n) { pkN()[i] = n; }
   DEVI int32_t getN(int i) const { return uni(pkN()[i]); }
   DEVI uint64_t getM(int i) const { return uni64(pkM()[i]); }
+  // shadow frames: + the lanes whose right-child box is hit (tested at the push) and the right child
+  DEVI void setFrameR(int i, int32_t n, uint64_t m, uint64_t r, int32_t c) {
+    pkN()[i] = n; pkM()[i] = m; pkR()[i] = r; pkC()[i] = c;
+  }
+  DEVI uint64_t getR(int i) const { return uni64(pkR()[i]); }
+  DEVI int32_t getC(int i) const { return uni(pkC()[i]); }
 };
 
 // accel_closest<INST = false> as a packet traversal (same per-lane semantics)
@@ -538,7 +553,13 @@ DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const
     if (N == INT32_MAX) return false;
   }
 }
-// accel_any<INST = false> as a packet traversal; a lane leaves the packet when blocked
+// accel_any<INST = false> as a packet traversal; a lane leaves the packet when blocked.
+// Both child boxes of a node are loaded (one scalar batch) and tested when it is pushed:
+// a box test is a pure function of (ray, box, dist), so testing the right box early
+// changes nothing but removes the unwind step's dependent scalar load. The frame keeps
+// the right child, the lanes in the node's subtree (M) and those whose right box is hit
+// (R); at the unwind the lanes still unblocked in R descend. The counting kernel counts
+// the right-box test at the unwind, for the lanes in M still unblocked, as accel_any does.
 template <bool CNT, uint32_t F>
 DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
   const RayInv ri = ray_inv(ao, ad, S.fastSlab);
@@ -559,13 +580,15 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
   while (true) {
     if (N >= 0) {  // internal: push (right child pending), go left with the lanes whose left box is hit
       const ChildBox cl = sload_child(S.node + N, 0);
-      st.setFrame(sp, N, act);
-      sp++;
-      bool hl = false;
+      const ChildBox cr = sload_child(S.node + N, 1);
+      bool hl = false, hr = false;
       if (in_mask(act)) {
         if (CNT) ct.c[C_NODE]++;
         hl = shadow_box<CNT>(cl.mn, cl.mx, ao, ad, ri, dist, ct);
+        hr = box_shadow(cr.mn, cr.mx, ao, ad, ri, dist);
       }
+      const uint64_t R = __ballot(hr);
+      if (CNT || R) st.setFrameR(sp++, 0, act, R, cr.ref);
       const uint64_t H = __ballot(hl);
       if (H) { act = H; N = cl.ref; continue; }
     } else if (N != INT32_MAX) {
@@ -578,13 +601,9 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
     N = INT32_MAX;
     while (sp > 0) {
       --sp;
-      const uint64_t M = st.getM(sp) & alive;
-      if (!M) continue;
-      const ChildBox cr = sload_child(S.node + st.getN(sp), 1);
-      bool hr = false;
-      if (in_mask(M)) hr = shadow_box<CNT>(cr.mn, cr.mx, ao, ad, ri, dist, ct);
-      const uint64_t R = __ballot(hr);
-      if (R) { act = R; N = cr.ref; break; }
+      if (CNT && in_mask(st.getM(sp) & alive)) ct.c[C_BOX]++;
+      const uint64_t R = st.getR(sp) & alive;
+      if (R) { act = R; N = st.getC(sp); break; }
     }
     if (N == INT32_MAX) return blocked;
   }
@@ -1323,6 +1342,19 @@ DEVI V disk_pos(const LightD& L, const Key& k, uint32_t kk) {  // getRandomDiskP
 }
 
 // calcShadowColor (myObjShader.java:98-153)
+// pow for shading terms: integer exponents 0..1024 by binary exponentiation (within ~20
+// ulps of pow for the phong exponents used; ocml's double pow is ~40x the instructions)
+DEVI double pow_shade(double x, double e) {
+  if (!(e >= 0 && e <= 1024 && e == floor(e))) return pow(x, e);
+  int n = (int)e;
+  double r = 1, b = x;
+  while (n) {
+    if (n & 1) r *= b;
+    n >>= 1;
+    if (n) b *= b;
+  }
+  return r;
+}
 template <bool CNT, uint32_t F>
 DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const Key& k, Counters& ct) {
   double r = 0, g = 0, b = 0;
@@ -1366,10 +1398,14 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     continue;
 #endif
     if (m.phong == 0) continue;
-    V hN = nrmz(mk(sr.d.x - h.dw.x, sr.d.y - h.dw.y, sr.d.z - h.dw.z));
-    double hdp = dot(hN, h.nrm) * ltMult;
+    // the specular term only adds colour (no hit / shadow / branch decision depends on it):
+    // it is evaluated to a few ulps instead of the reference's exact operation order --
+    // H normalised with one reciprocal, integer phong exponents by squaring
+    const V hv = mk(sr.d.x - h.dw.x, sr.d.y - h.dw.y, sr.d.z - h.dw.z);
+    const double hm = mag(hv), hr = hm == 0 ? 1.0 : 1.0 / hm;
+    double hdp = (hv.x * hr * h.nrm.x + hv.y * hr * h.nrm.y + hv.z * hr * h.nrm.z) * ltMult;
     if (hdp > EPS) {
-      double ph = pow(hdp * hdp, m.phong);
+      double ph = pow_shade(hdp * hdp, m.phong);
       r += m.specular[0] * L.color[0] * ph;
       g += m.specular[1] * L.color[1] * ph;
       b += m.specular[2] * L.color[2] * ph;
