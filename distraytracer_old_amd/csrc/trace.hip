@@ -452,6 +452,14 @@ int rt_time_render(rt_scene* s, const rt_render_params* p, int warmup, int iters
   return rc;
 }
 
+#ifdef RT_PROF_PKSTAT
+int rt_prof_pkstat_get(uint64_t* out) {  // profiling builds only: read and clear rt_pk_stat[8]
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(dv::rt_pk_stat), 8 * sizeof(uint64_t)));
+  const uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dv::rt_pk_stat), z, sizeof(z)));
+  return RT_OK;
+}
+#endif
 #ifdef RT_PROF_TIMELINE
 int rt_prof_timeline_set(void* d_buf) {  // profiling builds only
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dv::rt_tl_buf), &d_buf, sizeof(void*)));

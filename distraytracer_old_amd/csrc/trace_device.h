@@ -127,8 +127,14 @@ DEVI void renorm(WRay& r) {
   }
 }
 
+#ifdef RT_PROF_PKSTAT  // profiling builds only (tools/pkstat.py): packet-traversal lane utilisation
+// wave steps and the lanes testing in them: closest box / triangle, any-hit box / triangle
+enum { P_CB_STEP = C_N, P_CB_LANES, P_CT_STEP, P_CT_LANES, P_AB_STEP, P_AB_LANES, P_AT_STEP, P_AT_LANES, P_N };
+#else
+enum { P_N = C_N };
+#endif
 struct Counters {
-  uint64_t c[C_N];
+  uint64_t c[P_N];
 };
 
 // ---------------------------------------------------------------------------

@@ -115,6 +115,20 @@ DEVI uint64_t uni64(uint64_t v) {
   return ((uint64_t)(uint32_t)uni((int32_t)(v >> 32)) << 32) | (uint32_t)uni((int32_t)(uint32_t)v);
 }
 DEVI bool in_mask(uint64_t m) { return (m >> __lane_id()) & 1; }
+#ifdef RT_PROF_PKSTAT
+__device__ unsigned long long rt_pk_stat[8];
+// one wave step testing the lanes in m: counted once per wave (by its first active lane)
+#define PKSTAT(step, m)                                                                   \
+  do {                                                                                    \
+    const uint64_t pk_m_ = (m), pk_a_ = __ballot(1);                                      \
+    if (CNT && __lane_id() == (int)__builtin_ctzll(pk_a_)) {                              \
+      ct.c[step]++;                                                                       \
+      ct.c[step + 1] += __builtin_popcountll(pk_m_);                                      \
+    }                                                                                     \
+  } while (0)
+#else
+#define PKSTAT(step, m) do {} while (0)
+#endif
 
 // a primitive test whose triangle record is loaded at a wave-uniform address (PK)
 template <bool CNT, uint32_t F, bool PK, class LIM = LimNone>
@@ -175,6 +189,7 @@ DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRa
   const LeafR lf = leaf_of<PK>(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
   for (int i = 0; i < lf.count; ++i) {
+    if (PK) PKSTAT(P_CT_STEP, __ballot(1));
     int32_t ref = leaf_member<PK>(S, lf, i);
     renorm(w);  // _ray.getTransformedRay(_ray, obj.CTMara[invIDX])
     if constexpr (!INST && (F & FT_INST) != 0) {
@@ -374,6 +389,7 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
     while (N >= 0) {
       const ChildBox cl = sload_child(S.node + N, 0);
       st.setFrame(sp, N << 1, act);
+      PKSTAT(P_CB_STEP, act);
       bool hl = false;
       if (in_mask(act)) {
         if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }
@@ -394,6 +410,7 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
       const uint64_t M = st.getM(sp - 1);
       if ((np & 1) == 0) {
         const ChildBox cr = sload_child(S.node + (np >> 1), 1);
+        PKSTAT(P_CB_STEP, M);
         bool gr = false;
         if (in_mask(M)) gr = box_before(cr.mn, cr.mx, ao, ad, ri, local);
         const uint64_t R = __ballot(gr);
@@ -509,6 +526,7 @@ DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w
   const LeafR lf = leaf_of<PK>(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
   for (int i = 0; i < lf.count; ++i) {
+    if (PK) PKSTAT(P_AT_STEP, __ballot(1));
     int32_t ref = leaf_member<PK>(S, lf, i);
     renorm(w);
     if constexpr (!INST && (F & FT_INST) != 0) {
@@ -581,6 +599,7 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
     if (N >= 0) {  // internal: push (right child pending), go left with the lanes whose left box is hit
       const ChildBox cl = sload_child(S.node + N, 0);
       const ChildBox cr = sload_child(S.node + N, 1);
+      PKSTAT(P_AB_STEP, act);
       bool hl = false, hr = false;
       if (in_mask(act)) {
         if (CNT) ct.c[C_NODE]++;
@@ -1608,9 +1627,17 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
       WRay w;
       w.o = in.o; w.d = nrmz(in.d); w.d0 = w.d; w.stable = false; w.moved = false; w.ver = 0;  // myRay ctor
       k.node = in.node;
+#ifdef RT_PROF_NOTRACE  // profiling builds only (tools/variant_sweep.py): results differ
+      Best b = miss();
+#else
       Best b = closest<CNT, F, PACKET>(S, w, k, ct);
+#endif
       if (b.t == DMAX) {
         c = background<CNT, F>(S, w, ct);
+#ifdef RT_PROF_NOSHADE
+      } else if (true) {
+        c = mk(b.t * 0.01, 0, 0);
+#endif
       } else {
         HitRec h = make_hit<F>(S, b, w, k);
         bool branch;
@@ -1706,7 +1733,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   const bool valid = col < P.W && ri < P.nrows;
   Counters ct;
   if (CNT)
-    for (int i = 0; i < C_N; ++i) ct.c[i] = 0;
+    for (int i = 0; i < P_N; ++i) ct.c[i] = 0;
   const int row = P.row0 + (ri / P.band) * P.rowStep * P.band + ri % P.band;
   const double rayY = (-1 * (row - P.H / 2.0));
   const double rayX = col - P.W / 2.0;
@@ -1827,6 +1854,10 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   if (CNT) {
     for (int i = 0; i < C_N; ++i)
       if (ct.c[i]) atomicAdd(&gcount[i], (unsigned long long)ct.c[i]);
+#ifdef RT_PROF_PKSTAT
+    for (int i = C_N; i < P_N; ++i)
+      if (ct.c[i]) atomicAdd(&rt_pk_stat[i - C_N], (unsigned long long)ct.c[i]);
+#endif
   }
   if (!CNT && P.tcost && lane == 0) P.tcost[tile] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tl0);
 #ifdef RT_PROF_TIMELINE
@@ -1851,7 +1882,7 @@ __global__ void __launch_bounds__(64) probe_kernel(SceneD S, ParamsD P, uint32_t
   const int col = (t % tilesX) * P.tw, ri = (t / tilesX) * P.th;
   const int row = P.row0 + (ri / P.band) * P.rowStep * P.band + ri % P.band;
   Counters ct;
-  for (int i = 0; i < C_N; ++i) ct.c[i] = 0;
+  for (int i = 0; i < P_N; ++i) ct.c[i] = 0;
   WRay w;
   w.o = mk(0, 0, 0);
   w.d = nrmz(mk(col - P.W / 2.0, -1 * (row - P.H / 2.0), P.viewZ));

@@ -26,7 +26,10 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "nogather": ["RT_PROF_NOGATHER"],
     "knnheap": ["RT_KNN_HEAP"],
     "nophong": ["RT_PROF_NOPHONG"],
+    "noshade": ["RT_PROF_NOSHADE"],            # camera rays traced, no hit record / shading
+    "notrace": ["RT_PROF_NOTRACE"],            # camera rays generated, nothing traced
     "tl": ["RT_PROF_TIMELINE"],               # workgroup timeline (tools/timeline.py)
+    "pkstat": ["RT_PROF_PKSTAT"],             # packet lane utilisation (tools/pkstat.py)
 }
 FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS", "g": "RT_MAX_G", "p": "RT_PACKET",
           "l": "RT_PK_LDS"}
