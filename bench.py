@@ -8,7 +8,10 @@ workload C3 = scenes/c3_bun69k.cli (data/p3_t09.cli without `wood`) with the
 One step = one full C3 frame: every rank renders its rows (rank r renders the
 8-row bands r, r+N, r+2N, ... -- interleaved for load balance) with the HIP kernel into a
 device buffer, then (N>1) the per-rank float-RGB tiles are gathered to rank 0
-over RCCL (`dist.gather`: one point-to-point send per rank over xGMI). Work per step is one frame whatever N is
+over RCCL (`dist.gather`: one point-to-point send per rank over xGMI) and
+re-interleaved there; frame i's exchange overlaps frame i+1's render
+(`multigpu.FrameExchange`, double-buffered tiles) and the last one is drained
+inside the timed region. Work per step is one frame whatever N is
 (strong scaling). value = traced rays of the frame (camera + shadow + reflection
 + refraction, counted exactly by an instrumented run before timing) / max-over-
 ranks step time.
@@ -153,20 +156,22 @@ def main():
 
     rgb = torch.empty((maxrows, W, 3), dtype=torch.float32, device="cuda")
     argb = torch.empty((maxrows, W), dtype=torch.int32, device="cuda")
-    gathered = torch.empty((world, maxrows, W, 3), dtype=torch.float32, device="cuda") if dist and rank == 0 else None
     stream = torch.cuda.current_stream()
-    full_img = torch.empty((H, W, 3), dtype=torch.float32, device="cuda") if dist and rank == 0 else None
+    # N > 1: the single exchange -- float-RGB tiles gathered to rank 0 over RCCL and re-interleaved
+    # there -- pipelined against the next frame's render (multigpu.FrameExchange)
+    ex = multigpu.FrameExchange(dist, H, (maxrows, W, 3), "cuda") if dist else None
 
     def step(ev=None):
-        if ev:
-            ev[0].record(stream)
-        scene.render_device(p, rgb.data_ptr(), argb.data_ptr(), stream.cuda_stream)
-        if ev:
-            ev[1].record(stream)
-        if dist:  # the single exchange: float-RGB tiles to rank 0 over RCCL, re-interleaved there
-            multigpu.gather_tiles(rgb, dist, out=gathered)
-            if rank == 0:
-                full_img[:] = multigpu.assemble(gathered, H)
+        def render(tile):
+            if ev:
+                ev[0].record(stream)
+            scene.render_device(p, tile.data_ptr(), argb.data_ptr(), stream.cuda_stream)
+            if ev:
+                ev[1].record(stream)
+        if ex:
+            ex.step(render)
+        else:
+            render(rgb)
 
     # setup (untimed, like the counting run): a layout's first two renders calibrate its tile
     # dispatch order (probe, then measured wave times; rt_render_device in include/distraytracer.h)
@@ -175,6 +180,8 @@ def main():
     torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
+    if ex:
+        ex.finish()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -183,6 +190,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(evs[i])
+    if ex:
+        ex.finish()  # the last frame's gather + assemble are inside the timed region
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

@@ -60,6 +60,51 @@ def gather_tiles(tile, dist, group=None, dst: int = 0, out=None):
     return out if rank == dst else None
 
 
+class FrameExchange:
+    """Frames pipelined against their exchange: frame i renders into one of two tile buffers
+    while frame i-1's tile is still being gathered to rank 0 (an async `dist.gather`, which
+    RCCL runs on its own stream), so the xGMI transfer and rank 0's re-interleave overlap the
+    next frame's kernel instead of adding to it. Every frame is still gathered and assembled;
+    `finish()` drains the last one.
+
+      ex = FrameExchange(dist, H, (maxrows, W, 3), device)
+      for each frame: ex.step(lambda tile: render into tile)
+      ex.finish()                      # ex.image: the last assembled frame (rank 0)
+    """
+
+    def __init__(self, dist, H: int, tile_shape, device, dtype=None, band: int = BAND):
+        import torch
+
+        dtype = dtype or torch.float32
+        self.dist, self.H, self.band = dist, H, band
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.tiles = [torch.zeros(tuple(tile_shape), dtype=dtype, device=device) for _ in range(2)]
+        root = self.rank == 0
+        self.gathered = torch.empty((self.world,) + tuple(tile_shape), dtype=dtype, device=device) if root else None
+        self.image = torch.empty((H,) + tuple(tile_shape[1:]), dtype=dtype, device=device) if root else None
+        self.frame = 0
+        self._pending = None
+
+    def _complete(self):
+        if self._pending is not None:
+            self._pending.wait()  # NCCL: the current stream waits for the gather; gloo: the host does
+            self._pending = None
+            if self.rank == 0:
+                self.image.copy_(assemble(self.gathered, self.H, self.band))
+
+    def step(self, render):
+        tile = self.tiles[self.frame % 2]
+        render(tile)  # enqueued before the previous frame's gather is waited for: they overlap
+        self._complete()  # frame-1 gathered + assembled; its tile buffer is free again
+        outs = list(self.gathered.unbind(0)) if self.rank == 0 else None
+        self._pending = self.dist.gather(tile, outs, dst=0, async_op=True)
+        self.frame += 1
+
+    def finish(self):
+        self._complete()
+        return self.image
+
+
 def photon_shard(rank: int, world: int, count: int) -> tuple[int, int]:
     """Emitted-photon index range [first, first+n) of a rank (every light)."""
     first = rank * count // world

@@ -69,6 +69,50 @@ def test_gloo_world2_gather_equals_single_image():
     assert np.array_equal(full, ref)
 
 
+def _exchange_worker(rank, world, port, H, W, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    band = 2
+    rows = torch.tensor(multigpu.image_rows(rank, world, H, band), dtype=torch.float32)
+    maxrows = multigpu.max_tile_rows(world, H, band)
+    ex = multigpu.FrameExchange(dist, H, (maxrows, W, 1), "cpu", band=band)
+    seen = []
+    for f in range(4):
+        def render(tile, f=f):  # frame f's pixel value: 1000 * f + image row
+            tile.zero_()
+            tile[: len(rows), :, 0] = (1000 * f + rows)[:, None]
+        ex.step(render)
+        if rank == 0 and f > 0:
+            seen.append(ex.image[:, 0, 0].clone())  # frame f-1, assembled
+    last = ex.finish()
+    if rank == 0:
+        seen.append(last[:, 0, 0].clone())
+        q.put(torch.stack(seen).numpy())
+    else:
+        assert last is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world3_pipelined_exchange_delivers_every_frame():
+    """FrameExchange (bench.py's N-GPU step): frame i's gather overlaps frame i+1's render;
+    rank 0 still assembles every frame exactly, and finish() drains the last one."""
+    H, W, world = 13, 3, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_exchange_worker, args=(r, world, port, H, W, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    frames = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = np.stack([1000 * f + np.arange(H) for f in range(4)]).astype(np.float32)
+    assert np.array_equal(frames, expect)
+
+
 def test_assemble_numpy_ragged():
     for H, W, world, band in [(10, 3, 4, 1), (37, 5, 3, 4), (1024, 2, 8, 8), (19, 2, 8, 8)]:
         img = np.arange(H * W).reshape(H, W, 1)
