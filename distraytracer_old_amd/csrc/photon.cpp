@@ -8,7 +8,10 @@
 // leaves instead of chasing one dependent pointer per photon.
 //
 // Build: median partition of the photon index range on the axis of largest extent
-// (order by (coordinate, index)), boxes from the photons' exact coordinates.
+// (order by (coordinate, index)), boxes from the photons' exact coordinates; a leaf's
+// photons in id order. photon_build.hip builds the same structure on the GPU (the
+// default for maps above one leaf); this host build stays for tiny maps and as the
+// reference the device build is tested against (DISTRAYTRACER_PHOTON_BUILD=host).
 #include <algorithm>
 #include <cstring>
 #include <utility>
@@ -22,6 +25,7 @@ struct PhotonBvh {
   const std::vector<double>& pos;
   std::vector<int>& idx;
   std::vector<NodeD>& nodes;
+  std::vector<std::pair<int, int>> leaves;  // leaf ranges [lo, hi)
 
   void box(int lo, int hi, double* mn, double* mx) const {
     for (int c = 0; c < 3; ++c) { mn[c] = 1e300; mx[c] = -1e300; }
@@ -36,7 +40,10 @@ struct PhotonBvh {
   // Subtree over idx[lo, hi) as a child of its parent: a node index (>= 0), or -1 for a
   // leaf whose range the parent keeps in NodeD.pad (left: pad[0..1], right: pad[2..3]).
   int32_t build(int lo, int hi, bool force_node = false) {
-    if (hi - lo <= PHOTON_LEAF && !force_node) return -1;
+    if (hi - lo <= PHOTON_LEAF && !force_node) {
+      leaves.emplace_back(lo, hi);
+      return -1;
+    }
     double mn[3], mx[3];
     box(lo, hi, mn, mx);
     int ax = 0;
@@ -76,11 +83,15 @@ void build_photon_tree(HostScene& hs, const std::vector<double>& pos, const std:
   const int n = (int)(pos.size() / 3);
   hs.nphoton = n;
   hs.photonRoot = 0;
+  hs.pnodeCount = 0;
   if (n == 0) return;
   std::vector<int> idx(n);
   for (int i = 0; i < n; ++i) idx[i] = i;
-  PhotonBvh b{pos, idx, hs.pnode};
+  PhotonBvh b{pos, idx, hs.pnode, {}};
   hs.photonRoot = b.build(0, n, true);  // the root is always a node
+  hs.pnodeCount = (int64_t)hs.pnode.size();
+  // photons of a leaf in id order (deterministic; the same as the device build, photon_build.hip)
+  for (auto& lf : b.leaves) std::sort(idx.begin() + lf.first, idx.begin() + lf.second);
   hs.ppos.resize(3 * (size_t)n);
   hs.ppwr.resize(3 * (size_t)n);
   for (int i = 0; i < n; ++i)

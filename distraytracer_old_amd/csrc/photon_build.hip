@@ -1,0 +1,339 @@
+// GPU build of the photon-map search structure: the same median BVH as the host builder
+// (csrc/photon.cpp, which documents the structure), level by level on the device.
+//
+// The host recursion splits each photon range [lo, hi) (> PHOTON_LEAF photons, or the root)
+// at mid = lo + (hi - lo) / 2 on the axis of largest extent, the left half being the
+// (mid - lo) smallest photons in (coordinate, photon index) order. Here:
+//  * three lists hold the photon ids sorted by (x, id), (y, id), (z, id) -- one stable
+//    radix sort each, the key being the coordinate + 0.0 (so -0 == +0, as the host's
+//    comparator treats them);
+//  * every list stays sorted within each range, so a range's box is read from the first
+//    and last entries of the three lists, and its left half is the first (mid - lo)
+//    entries of the split axis' list;
+//  * one level = all ranges of one depth: flag the left halves, then stably partition each
+//    list within its ranges (an exclusive scan of the flags gives every entry's place).
+// Node numbering is the host's DFS pre-order: the number of internal nodes under a range
+// depends on its photon count only (T(c) = 0 for c <= PHOTON_LEAF, else 1 + T(c/2) +
+// T(c - c/2)), so a right child is numbered parent + 1 + T(left count). Leaf photons are
+// ordered by photon id (as the host's leaves are), so both builders produce the same
+// nodes, boxes and leaf-ordered photon arrays: images are bit-identical.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <hipcub/hipcub.hpp>
+#include <map>
+
+#include "rt_internal.h"
+
+namespace rt {
+namespace pb {
+
+struct Range {
+  int32_t lo, cnt;
+  int32_t parent;  // node whose child this range is (-1: the root)
+  int32_t side;    // 0 left, 1 right
+  int32_t node;    // this range's node (DFS pre-order), -1 when it is a leaf
+  int32_t axis, mid, pad;
+};
+
+static constexpr int TMAX = 128;
+struct TTable {  // T(c) for the <= 2 counts per level
+  int32_t n;
+  int32_t c[TMAX];
+  int32_t t[TMAX];
+};
+
+__device__ inline int32_t t_of(const TTable& T, int32_t c) {
+  if (c <= PHOTON_LEAF) return 0;
+  for (int i = 0; i < T.n; ++i)
+    if (T.c[i] == c) return T.t[i];
+  return -1;  // not reached: the host tabulates every count of the tree
+}
+
+__global__ void k_keys(const double* __restrict__ pos, int32_t n, int c, double* __restrict__ key,
+                       int32_t* __restrict__ id) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  key[i] = pos[3 * (size_t)i + c] + 0.0;
+  id[i] = i;
+}
+
+// One thread per range: its box (from the sorted lists) and reference go into its parent;
+// an internal range also fills its own node's ranges and picks its split.
+__global__ void k_ranges(const double* __restrict__ pos, const int32_t* __restrict__ L0, const int32_t* __restrict__ L1,
+                         const int32_t* __restrict__ L2, Range* __restrict__ rg, int32_t nr, NodeD* __restrict__ nodes,
+                         int32_t* __restrict__ internal, int32_t* __restrict__ leafStart) {
+  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nr) return;
+  Range R = rg[r];
+  const int32_t* L[3] = {L0, L1, L2};
+  double mn[3], mx[3];
+  for (int c = 0; c < 3; ++c) {
+    mn[c] = pos[3 * (size_t)L[c][R.lo] + c];
+    mx[c] = pos[3 * (size_t)L[c][R.lo + R.cnt - 1] + c];
+  }
+  if (R.parent >= 0) {
+    NodeD& P = nodes[R.parent];
+    double* bmn = R.side ? P.rmin : P.lmin;
+    double* bmx = R.side ? P.rmax : P.lmax;
+    for (int c = 0; c < 3; ++c) { bmn[c] = mn[c]; bmx[c] = mx[c]; }
+    if (R.side) P.right = R.node;
+    else P.left = R.node;
+  }
+  internal[r] = R.node >= 0;
+  if (R.node < 0) {
+    leafStart[R.lo] = R.cnt;
+    return;
+  }
+  int ax = 0;
+  for (int c = 1; c < 3; ++c)
+    if (mx[c] - mn[c] > mx[ax] - mn[ax]) ax = c;
+  const int32_t mid = R.lo + R.cnt / 2;
+  NodeD& N = nodes[R.node];
+  N.pad[0] = R.lo; N.pad[1] = mid - R.lo;
+  N.pad[2] = mid; N.pad[3] = R.lo + R.cnt - mid;
+  N.pad[4] = R.cnt;
+  N.pad[5] = 0;
+  rg[r].axis = ax;
+  rg[r].mid = mid;
+}
+
+// the two children of every internal range, in range order (so the next level stays sorted by lo)
+__global__ void k_children(const Range* __restrict__ rg, int32_t nr, const int32_t* __restrict__ base,
+                           Range* __restrict__ next, TTable T) {
+  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nr) return;
+  const Range R = rg[r];
+  if (R.node < 0) return;
+  const int32_t lc = R.mid - R.lo, rc = R.cnt - lc;
+  Range a{R.lo, lc, R.node, 0, lc > PHOTON_LEAF ? R.node + 1 : -1, 0, 0, 0};
+  Range b{R.mid, rc, R.node, 1, rc > PHOTON_LEAF ? R.node + 1 + t_of(T, lc) : -1, 0, 0, 0};
+  next[2 * base[r]] = a;
+  next[2 * base[r] + 1] = b;
+}
+
+// range of list position p at this level (-1: p lies in a leaf finished earlier)
+__device__ inline int32_t range_of(const Range* rg, int32_t nr, int32_t p) {
+  int32_t a = 0, b = nr - 1;
+  while (a < b) {  // last range with lo <= p
+    const int32_t m = (a + b + 1) >> 1;
+    if (rg[m].lo <= p) a = m;
+    else b = m - 1;
+  }
+  const Range& R = rg[a];
+  return (R.lo <= p && p < R.lo + R.cnt && R.node >= 0) ? a : -1;
+}
+
+__global__ void k_locate(const Range* __restrict__ rg, int32_t nr, int32_t n, int32_t* __restrict__ posRange) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  posRange[p] = range_of(rg, nr, p);
+}
+
+// left[id] for the photons of internal ranges: the first (mid - lo) entries of the split axis' list
+__global__ void k_mark(const Range* __restrict__ rg, const int32_t* __restrict__ posRange, int32_t n,
+                       const int32_t* __restrict__ L0, const int32_t* __restrict__ L1, const int32_t* __restrict__ L2,
+                       uint8_t* __restrict__ left) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int32_t r = posRange[p];
+  if (r < 0) return;
+  const Range& R = rg[r];
+  const int32_t* L = R.axis == 0 ? L0 : (R.axis == 1 ? L1 : L2);
+  left[L[p]] = p < R.mid;
+}
+
+__global__ void k_flags(const int32_t* __restrict__ posRange, int32_t n, const int32_t* __restrict__ L,
+                        const uint8_t* __restrict__ left, int32_t* __restrict__ f) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  f[p] = posRange[p] >= 0 ? left[L[p]] : 0;
+}
+
+// stable partition of one list within every internal range (scan = exclusive sum of the flags)
+__global__ void k_scatter(const Range* __restrict__ rg, const int32_t* __restrict__ posRange, int32_t n,
+                          const int32_t* __restrict__ L, const int32_t* __restrict__ scan, const int32_t* __restrict__ f,
+                          int32_t* __restrict__ out) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int32_t r = posRange[p];
+  int32_t q = p;
+  if (r >= 0) {
+    const Range& R = rg[r];
+    const int32_t before = scan[p] - scan[R.lo];  // left entries of this range before p
+    q = f[p] ? R.lo + before : R.mid + (p - R.lo) - before;
+  }
+  out[q] = L[p];
+}
+
+// leaves: photons ordered by id; then the leaf-ordered position / power arrays
+__global__ void k_leaf_order(const int32_t* __restrict__ leafStart, int32_t n, int32_t* __restrict__ L) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int32_t c = leafStart[p];
+  for (int32_t i = p + 1; i < p + c; ++i) {  // insertion sort of <= PHOTON_LEAF ids
+    const int32_t v = L[i];
+    int32_t j = i - 1;
+    while (j >= p && L[j] > v) { L[j + 1] = L[j]; --j; }
+    L[j + 1] = v;
+  }
+}
+
+__global__ void k_gather(const int32_t* __restrict__ L, int32_t n, const double* __restrict__ pos,
+                         const double* __restrict__ pwr, double* __restrict__ ppos, double* __restrict__ ppwr) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const size_t s = 3 * (size_t)L[p], d = 3 * (size_t)p;
+  for (int c = 0; c < 3; ++c) { ppos[d + c] = pos[s + c]; ppwr[d + c] = pwr[s + c]; }
+}
+
+// internal nodes of the median tree over c photons (the root of a map is always a node)
+static int64_t t_count(int64_t c, std::map<int64_t, int64_t>& memo) {
+  if (c <= PHOTON_LEAF) return 0;
+  auto it = memo.find(c);
+  if (it != memo.end()) return it->second;
+  const int64_t v = 1 + t_count(c / 2, memo) + t_count(c - c / 2, memo);
+  memo[c] = v;
+  return v;
+}
+
+struct DevBuf {  // scratch allocations of one build, freed on every path
+  std::vector<void*> p;
+  template <class T>
+  hipError_t alloc(T** out, size_t count) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
+    if (e == hipSuccess) p.push_back(q);
+    *out = (T*)q;
+    return e;
+  }
+  ~DevBuf() {
+    for (void* q : p) (void)hipFree(q);
+  }
+};
+
+}  // namespace pb
+
+#define PBCHK(x)                                                                              \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) return set_error(RT_E_HIP, std::string("photon map build: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+// Build the photon map of photon_list (pos / pwr, insertion order) on the scene's device.
+// out: device arrays owned by the scene (allocs); n > PHOTON_LEAF.
+int build_photon_tree_gpu(rt_scene* s, const double* pos_h, const double* pwr_h, int64_t n64) {
+  using namespace pb;
+  const int32_t n = (int32_t)n64;
+  const int TB = 256;
+  const unsigned gn = (unsigned)((n + TB - 1) / TB);
+  std::map<int64_t, int64_t> memo;
+  const int64_t nnodes = t_count(n, memo);
+  TTable T{};
+  for (auto& kv : memo) {
+    if (T.n >= TMAX) return set_error(RT_E_INVALID, "photon map build: count table overflow");
+    T.c[T.n] = (int32_t)kv.first;
+    T.t[T.n] = (int32_t)kv.second;
+    ++T.n;
+  }
+  DevBuf tmp;
+  double *pos, *pwr, *key, *keyAlt;
+  int32_t *id, *L[3], *Lalt, *posRange, *f, *scan, *leafStart, *internal, *base;
+  uint8_t* left;
+  Range *rg, *next;
+  const size_t maxRanges = (size_t)n / (PHOTON_LEAF / 2) + 4;
+  PBCHK(tmp.alloc(&pos, 3 * (size_t)n));
+  PBCHK(tmp.alloc(&pwr, 3 * (size_t)n));
+  PBCHK(tmp.alloc(&key, n));
+  PBCHK(tmp.alloc(&keyAlt, n));
+  PBCHK(tmp.alloc(&id, n));
+  for (int c = 0; c < 3; ++c) PBCHK(tmp.alloc(&L[c], n));
+  PBCHK(tmp.alloc(&Lalt, n));
+  PBCHK(tmp.alloc(&posRange, n));
+  PBCHK(tmp.alloc(&f, n));
+  PBCHK(tmp.alloc(&scan, n));
+  PBCHK(tmp.alloc(&leafStart, n));
+  PBCHK(tmp.alloc(&left, n));
+  PBCHK(tmp.alloc(&rg, maxRanges));
+  PBCHK(tmp.alloc(&next, maxRanges));
+  PBCHK(tmp.alloc(&internal, maxRanges));
+  PBCHK(tmp.alloc(&base, maxRanges));
+  // results (scene-owned)
+  NodeD* nodes = nullptr;
+  double *ppos = nullptr, *ppwr = nullptr;
+  PBCHK(hipMalloc(&nodes, sizeof(NodeD) * nnodes));
+  s->allocs.push_back(nodes);
+  PBCHK(hipMalloc(&ppos, sizeof(double) * 3 * (size_t)n));
+  s->allocs.push_back(ppos);
+  PBCHK(hipMalloc(&ppwr, sizeof(double) * 3 * (size_t)n));
+  s->allocs.push_back(ppwr);
+  s->devBytes += sizeof(NodeD) * nnodes + 2 * sizeof(double) * 3 * (size_t)n;
+  PBCHK(hipMemset(nodes, 0, sizeof(NodeD) * nnodes));
+  PBCHK(hipMemset(leafStart, 0, sizeof(int32_t) * n));
+  PBCHK(hipMemcpy(pos, pos_h, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice));
+  PBCHK(hipMemcpy(pwr, pwr_h, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice));
+  // scratch of the library primitives (sized for the largest call)
+  size_t sortBytes = 0, scanBytes = 0, scanBytesR = 0;
+  PBCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sortBytes, key, keyAlt, id, L[0], n));
+  PBCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scanBytes, f, scan, n));
+  PBCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scanBytesR, internal, base, (int)maxRanges));
+  void* cub = nullptr;
+  PBCHK(tmp.alloc((char**)&cub, std::max(sortBytes, std::max(scanBytes, scanBytesR))));
+  // the three (coordinate, id) orders
+  for (int c = 0; c < 3; ++c) {
+    hipLaunchKernelGGL(k_keys, dim3(gn), dim3(TB), 0, 0, pos, n, c, key, id);
+    PBCHK(hipGetLastError());
+    size_t b = sortBytes;
+    PBCHK(hipcub::DeviceRadixSort::SortPairs(cub, b, key, keyAlt, id, L[c], n));
+  }
+  // level by level
+  Range root{0, n, -1, 0, 0, 0, 0, 0};
+  PBCHK(hipMemcpy(rg, &root, sizeof(Range), hipMemcpyHostToDevice));
+  int32_t nr = 1;
+  while (nr > 0) {
+    const unsigned gr = (unsigned)((nr + TB - 1) / TB);
+    hipLaunchKernelGGL(k_ranges, dim3(gr), dim3(TB), 0, 0, pos, L[0], L[1], L[2], rg, nr, nodes, internal, leafStart);
+    PBCHK(hipGetLastError());
+    size_t b = scanBytesR;
+    PBCHK(hipcub::DeviceScan::ExclusiveSum(cub, b, internal, base, nr));
+    int32_t lastBase = 0, lastInt = 0;
+    PBCHK(hipMemcpy(&lastBase, base + nr - 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+    PBCHK(hipMemcpy(&lastInt, internal + nr - 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+    const int32_t nint = lastBase + lastInt;
+    if (nint == 0) break;
+    if ((size_t)2 * nint > maxRanges) return set_error(RT_E_INVALID, "photon map build: range overflow");
+    hipLaunchKernelGGL(k_children, dim3(gr), dim3(TB), 0, 0, rg, nr, base, next, T);
+    hipLaunchKernelGGL(k_locate, dim3(gn), dim3(TB), 0, 0, rg, nr, n, posRange);
+    hipLaunchKernelGGL(k_mark, dim3(gn), dim3(TB), 0, 0, rg, posRange, n, L[0], L[1], L[2], left);
+    PBCHK(hipGetLastError());
+    for (int c = 0; c < 3; ++c) {
+      hipLaunchKernelGGL(k_flags, dim3(gn), dim3(TB), 0, 0, posRange, n, L[c], left, f);
+      size_t bs = scanBytes;
+      PBCHK(hipcub::DeviceScan::ExclusiveSum(cub, bs, f, scan, n));
+      hipLaunchKernelGGL(k_scatter, dim3(gn), dim3(TB), 0, 0, rg, posRange, n, L[c], scan, f, Lalt);
+      PBCHK(hipGetLastError());
+      std::swap(L[c], Lalt);
+    }
+    std::swap(rg, next);
+    nr = 2 * nint;
+  }
+  hipLaunchKernelGGL(k_leaf_order, dim3(gn), dim3(TB), 0, 0, leafStart, n, L[0]);
+  hipLaunchKernelGGL(k_gather, dim3(gn), dim3(TB), 0, 0, L[0], n, pos, pwr, ppos, ppwr);
+  PBCHK(hipGetLastError());
+  PBCHK(hipDeviceSynchronize());
+  s->dev.pnode = nodes;
+  s->dev.ppos = ppos;
+  s->dev.ppwr = ppwr;
+  s->dev.nphoton = n;
+  s->dev.photonRoot = 0;
+  s->hs.pnode.clear();
+  s->hs.ppos.clear();
+  s->hs.ppwr.clear();
+  s->hs.photonRoot = 0;
+  s->hs.nphoton = n;
+  s->hs.pnodeCount = nnodes;
+  s->photonsUploaded = true;
+  return RT_OK;
+}
+
+}  // namespace rt

@@ -32,6 +32,7 @@ struct HostScene {
   std::vector<double> photonListPos, photonListPwr;
   int photonRoot = 0;
   int64_t nphoton = 0;
+  int64_t pnodeCount = 0;  // photon-map nodes (host- or device-built)
   // scene parameters
   double fov = 60;
   double bg[3] = {0, 0, 0};
@@ -52,6 +53,12 @@ int build_host_scene(const rt_scene_desc* d, HostScene& hs);  // scene_build.cpp
 // photon.cpp: photon-map search structure from the photon_list in insertion order
 void build_photon_tree(HostScene& hs, const std::vector<double>& pos, const std::vector<double>& pwr);
 
+}  // namespace rt
+
+struct rt_scene;
+namespace rt {
+// photon_build.hip: the same structure built on the scene's device (n > PHOTON_LEAF)
+int build_photon_tree_gpu(rt_scene* s, const double* pos, const double* pwr, int64_t n);
 }  // namespace rt
 
 struct rt_scene {

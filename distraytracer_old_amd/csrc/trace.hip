@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <mutex>
@@ -528,6 +529,24 @@ static int check_photon_params(const HostScene& h) {
   return RT_OK;
 }
 
+// The photon map of photon_list: built on the device (photon_build.hip) unless it fits one
+// leaf or DISTRAYTRACER_PHOTON_BUILD=host asks for the host build (csrc/photon.cpp; the two
+// are identical -- a GPU test checks it).
+static int set_photon_map(rt_scene* s, std::vector<double>& pos, std::vector<double>& pwr) {
+  HostScene& h = s->hs;
+  const int64_t n = (int64_t)(pos.size() / 3);
+  const char* mode = std::getenv("DISTRAYTRACER_PHOTON_BUILD");
+  if (n > PHOTON_LEAF && !(mode && std::string(mode) == "host")) {
+    HIPCHK(hipSetDevice(s->device));
+    int rc = build_photon_tree_gpu(s, pos.data(), pwr.data(), n);
+    h.photonListPos.swap(pos);
+    h.photonListPwr.swap(pwr);
+    return rc;
+  }
+  build_photon_tree(h, pos, pwr);
+  return rt_upload_photons(s);
+}
+
 extern "C" int rt_photons_build(rt_scene* s, uint64_t seed) {
   if (!s) return set_error(RT_E_INVALID, "null scene");
   HostScene& h = s->hs;
@@ -537,8 +556,7 @@ extern "C" int rt_photons_build(rt_scene* s, uint64_t seed) {
   std::vector<double> pos, pwr;
   std::vector<int64_t> perLight;
   if ((rc = shoot_photons(s, seed, 0, h.photonCount, pos, pwr, perLight))) return rc;
-  build_photon_tree(h, pos, pwr);
-  return rt_upload_photons(s);
+  return set_photon_map(s, pos, pwr);
 }
 
 extern "C" int rt_photons_shoot(rt_scene* s, uint64_t seed, int64_t first, int64_t count, int64_t* per_light) {
@@ -565,7 +583,21 @@ extern "C" int rt_photons_set(rt_scene* s, const double* pos, const double* pwr,
   if (rc) return rc;
   if (n > INT32_MAX / 4) return set_error(RT_E_INVALID, "photon map too large");
   std::vector<double> p(pos, pos + 3 * n), w(pwr, pwr + 3 * n);
-  build_photon_tree(h, p, w);
   s->photonsUploaded = false;
-  return rt_upload_photons(s);
+  return set_photon_map(s, p, w);
+}
+
+extern "C" int rt_scene_photon_map(const rt_scene* s, void* nodes, int64_t node_cap, double* ppos, double* ppwr,
+                                   int64_t n, int64_t* n_nodes, int32_t* root) {
+  if (!s || !n_nodes) return set_error(RT_E_INVALID, "null argument");
+  const HostScene& h = s->hs;
+  *n_nodes = h.pnodeCount;
+  if (root) *root = s->dev.photonRoot;
+  if (!s->photonsUploaded) return RT_OK;
+  HIPCHK(hipSetDevice(s->device));
+  const int64_t nn = std::min<int64_t>(node_cap, h.pnodeCount), np = std::min<int64_t>(n, h.nphoton);
+  if (nodes && nn > 0) HIPCHK(hipMemcpy(nodes, s->dev.pnode, sizeof(NodeD) * nn, hipMemcpyDeviceToHost));
+  if (ppos && np > 0) HIPCHK(hipMemcpy(ppos, s->dev.ppos, sizeof(double) * 3 * np, hipMemcpyDeviceToHost));
+  if (ppwr && np > 0) HIPCHK(hipMemcpy(ppwr, s->dev.ppwr, sizeof(double) * 3 * np, hipMemcpyDeviceToHost));
+  return RT_OK;
 }

@@ -39,7 +39,8 @@ class RenderParams(ctypes.Structure):
 EXPORTS = ["rt_abi_version", "rt_last_error", "rt_device_count", "rt_scene_create", "rt_scene_load_cli",
            "rt_scene_inspect_cli",
            "rt_scene_info", "rt_scene_destroy", "rt_photons_build", "rt_render", "rt_render_device",
-           "rt_render_count", "rt_time_render", "rt_scene_photons", "rt_photons_shoot", "rt_photons_set",
+           "rt_render_count", "rt_time_render", "rt_scene_photons", "rt_scene_photon_map", "rt_photons_shoot",
+           "rt_photons_set",
            "rt_png_name", "rt_scene_save_name"]
 
 _lib = None
@@ -72,6 +73,9 @@ def lib():
         L.rt_photons_build.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         L.rt_scene_photons.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                        ctypes.POINTER(ctypes.c_int64)]
+        L.rt_scene_photon_map.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                                          ctypes.POINTER(ctypes.c_int32)]
         L.rt_photons_shoot.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
         L.rt_photons_set.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         L.rt_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_void_p]
@@ -188,6 +192,19 @@ class Scene:
         pos = np.ascontiguousarray(pos, dtype=np.float64)
         pwr = np.ascontiguousarray(pwr, dtype=np.float64)
         _check(lib().rt_photons_set(self._h, pos.ctypes.data, pwr.ctypes.data, len(pos)), "rt_photons_set")
+
+    def photon_map(self):
+        """The device photon map: (nodes as raw uint8 [n_nodes, 128], root, ppos [n,3], ppwr [n,3])."""
+        nn = ctypes.c_int64(0)
+        root = ctypes.c_int32(0)
+        _check(lib().rt_scene_photon_map(self._h, None, 0, None, None, 0, ctypes.byref(nn), ctypes.byref(root)),
+               "rt_scene_photon_map")
+        n = self.info()["photons"]
+        nodes = np.zeros((nn.value, 128), dtype=np.uint8)
+        ppos = np.zeros((n, 3)); ppwr = np.zeros((n, 3))
+        _check(lib().rt_scene_photon_map(self._h, nodes.ctypes.data, nn.value, ppos.ctypes.data, ppwr.ctypes.data, n,
+                                         ctypes.byref(nn), ctypes.byref(root)), "rt_scene_photon_map")
+        return nodes, root.value, ppos, ppwr
 
     def photons(self):
         """(pos [n,3], pwr [n,3]) of the photon map in photon_list insertion order."""

@@ -214,6 +214,13 @@ int rt_photons_build(rt_scene* scene, uint64_t seed);
    insertion order): *count = number of photons; copies min(n, count) positions / powers
    (double[3] each) to pos / pwr. */
 int rt_scene_photons(const rt_scene* scene, double* pos, double* pwr, int64_t n, int64_t* count);
+/* The photon map's search structure as the device holds it (inspection / tests): *n_nodes = its
+   node count (NodeD records of 128 bytes, csrc/rt_types.h), *root = the root node; copies up to
+   node_cap records to nodes and up to n leaf-ordered positions / powers (double[3]) to ppos / ppwr
+   (any of them may be NULL). Built on the GPU (photon_build.hip) or, for a map of one leaf or with
+   DISTRAYTRACER_PHOTON_BUILD=host in the environment, on the host (photon.cpp): the same structure. */
+int rt_scene_photon_map(const rt_scene* scene, void* nodes, int64_t node_cap, double* ppos, double* ppwr, int64_t n,
+                        int64_t* n_nodes, int32_t* root);
 /* Sharded pre-pass (multi-GPU): shoot only emitted photons [first, first+count) of
    every light (same keyed RNG, so the union of shards is the full pre-pass); the scene's
    photon_list becomes that shard (light-major, then photon index, then path order) without a

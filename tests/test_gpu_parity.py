@@ -221,3 +221,56 @@ def test_tile_schedule_does_not_change_the_image():
     for _ in range(3):  # probe order + measuring, then measured order twice
         a, aa = g.render(512, 512, spp=2, seed=SEED)
         assert np.array_equal(aa, ab) and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def _maps_equal(a, b):
+    """Two photon maps (Scene.photon_map()) are the same structure: node refs / ranges / counts
+    bit-equal, boxes equal as numbers (a box bound's zero may carry either sign), leaf-ordered
+    photons bit-equal."""
+    na, ra, pa, wa = a
+    nb, rb, pb, wb = b
+    assert na.shape == nb.shape and ra == rb
+    assert np.array_equal(na[:, 96:], nb[:, 96:])  # left, right, pad[6]
+    assert np.array_equal(na[:, :96].view(np.float64), nb[:, :96].view(np.float64))
+    assert np.array_equal(pa.view(np.uint64), pb.view(np.uint64)) and np.array_equal(wa.view(np.uint64), wb.view(np.uint64))
+
+
+def test_gpu_photon_map_build_equals_host_build(tmp_path, monkeypatch):
+    """The photon map's search structure built on the GPU (photon_build.hip, the default) is the
+    host build's (photon.cpp) node for node, and renders the same image bit for bit."""
+    src = (scenes.SCENE_DIR / "t11.cli").read_text().replace("diffuse_photons  1000000  200 0.1",
+                                                             "diffuse_photons  60000  50 0.1")
+    (tmp_path / "t11m.cli").write_text(src)
+    seed = 0x5EED0005
+    g = rt.Scene.load_cli("t11m.cli", scene_dir=tmp_path, textures={})
+    g.build_photons(seed)
+    monkeypatch.setenv("DISTRAYTRACER_PHOTON_BUILD", "host")
+    h = rt.Scene.load_cli("t11m.cli", scene_dir=tmp_path, textures={})
+    h.build_photons(seed)
+    monkeypatch.delenv("DISTRAYTRACER_PHOTON_BUILD")
+    assert g.info()["photons"] > 1000
+    _maps_equal(g.photon_map(), h.photon_map())
+    a = g.render(64, 64, spp=2, seed=seed)
+    b = h.render(64, 64, spp=2, seed=seed)
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+
+
+@pytest.mark.parametrize("n", [25, 49, 1000, 262147])
+def test_gpu_photon_map_build_ties_and_sizes(tmp_path, monkeypatch, n):
+    """Adversarial photon lists through rt_photons_set: heavy coordinate ties (a coarse grid),
+    signed zeros, a range straddling one leaf -- GPU build == host build."""
+    (tmp_path / "t11m.cli").write_text((scenes.SCENE_DIR / "t11.cli").read_text())
+    rng = np.random.default_rng(n)
+    pos = rng.integers(-3, 4, size=(n, 3)).astype(np.float64) * 0.25
+    pos[rng.random((n, 3)) < 0.2] = -0.0
+    pwr = rng.random((n, 3))
+    maps = []
+    for mode in ("gpu", "host"):
+        if mode == "host":
+            monkeypatch.setenv("DISTRAYTRACER_PHOTON_BUILD", "host")
+        s = rt.Scene.load_cli("t11m.cli", scene_dir=tmp_path, textures={})
+        s.set_photons(pos, pwr)
+        maps.append(s.photon_map())
+        s.close()
+    monkeypatch.delenv("DISTRAYTRACER_PHOTON_BUILD")
+    _maps_equal(maps[0], maps[1])
