@@ -38,7 +38,7 @@ struct PhotonBvh {
     }
   }
   // Subtree over idx[lo, hi) as a child of its parent: a node index (>= 0), or -1 for a
-  // leaf whose range the parent keeps in NodeD.pad (left: pad[0..1], right: pad[2..3]).
+  // leaf whose range the parent keeps in NodeD.pad (left: pad[0..1], right: pad[2], padR[0]).
   int32_t build(int lo, int hi, bool force_node = false) {
     if (hi - lo <= PHOTON_LEAF && !force_node) {
       leaves.emplace_back(lo, hi);
@@ -66,8 +66,8 @@ struct PhotonBvh {
     nd.left = l;
     nd.right = r;
     nd.pad[0] = lo; nd.pad[1] = mid - lo;
-    nd.pad[2] = mid; nd.pad[3] = hi - mid;
-    nd.pad[4] = hi - lo;  // photons in the subtree
+    nd.pad[2] = mid; nd.padR[0] = hi - mid;
+    nd.padR[1] = hi - lo;  // photons in the subtree
     return me;
   }
 };

@@ -91,9 +91,9 @@ __global__ void k_ranges(const double* __restrict__ pos, const int32_t* __restri
   const int32_t mid = R.lo + R.cnt / 2;
   NodeD& N = nodes[R.node];
   N.pad[0] = R.lo; N.pad[1] = mid - R.lo;
-  N.pad[2] = mid; N.pad[3] = R.lo + R.cnt - mid;
-  N.pad[4] = R.cnt;
-  N.pad[5] = 0;
+  N.pad[2] = mid; N.padR[0] = R.lo + R.cnt - mid;
+  N.padR[1] = R.cnt;
+  N.padR[2] = 0;
   rg[r].axis = ax;
   rg[r].mid = mid;
 }

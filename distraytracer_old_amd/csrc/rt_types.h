@@ -51,12 +51,18 @@ struct PrimD {
 };
 
 // BVH node with both child boxes (reference topology, myBVH.addObjList
-// myGeomBase.java:360-386). child >= 0: node index; child < 0: leaf ~index. 128 B.
+// myGeomBase.java:360-386). child >= 0: node index; child < 0: leaf ~index. 128 B =
+// two 64-B lines, one per child (box + reference): a descent step reads only the
+// left child's line, an unwind step only the right child's.
 struct NodeD {
-  double lmin[3], lmax[3], rmin[3], rmax[3];
-  int32_t left, right;
-  int32_t pad[6];
+  double lmin[3], lmax[3];
+  int32_t left;
+  int32_t pad[3];   // photon map: left child range (start, count), right child start
+  double rmin[3], rmax[3];
+  int32_t right;
+  int32_t padR[3];  // photon map: right child count, photons in the subtree
 };
+static_assert(sizeof(NodeD) == 128, "NodeD is two 64-B lines");
 struct LeafD {
   int32_t start, count;  // range in leaf member refs (>= 0 tri index, < 0 ~prim index)
 };
@@ -116,7 +122,7 @@ struct TexD {
 
 // Photon map (myKD_Tree of myPhoton, myLight.java:278-446) on the device: a BVH over the
 // photons (NodeD records; child ref >= 0 node, -1 leaf whose photon range [start,
-// start+count) is in pad[0..1] (left) / pad[2..3] (right); <= 24 photons per leaf) with
+// start+count) is in pad[0..1] (left) / pad[2], padR[0] (right); <= 24 photons per leaf) with
 // the photon positions and powers as double[3] arrays in leaf order (csrc/photon.cpp). The k-nearest set a query finds does not depend on the
 // search structure, so this replaces the reference's one-photon-per-node kd-tree.
 static constexpr int PHOTON_LEAF = 24;

@@ -1106,7 +1106,7 @@ DEVI V irradiance_heap(const SceneD& S, V p, Counters& ct) {
       const int32_t child = side ? pn.right : pn.left;
       if (child >= 0) { N = child; break; }
       // leaf: scan its photons
-      const int start = side ? pn.pad[2] : pn.pad[0], count = side ? pn.pad[3] : pn.pad[1];
+      const int start = side ? pn.pad[2] : pn.pad[0], count = side ? pn.padR[0] : pn.pad[1];
       if (CNT) ct.c[C_PHOTON] += count;
       for (int q = 0; q < count; ++q) {
         const double* ph = S.ppos + 3 * (size_t)(start + q);
@@ -1167,7 +1167,7 @@ DEVI void photon_scan(const SceneD& S, const double* pos, double R2, Counters& c
       if (!(box_d2(mn, mx, pos) < R2)) continue;
       const int32_t c = side ? nd.right : nd.left;
       if (c >= 0) { st.setN(sp++, c); continue; }
-      const int start = side ? nd.pad[2] : nd.pad[0], count = side ? nd.pad[3] : nd.pad[1];
+      const int start = side ? nd.pad[2] : nd.pad[0], count = side ? nd.padR[0] : nd.pad[1];
       if (CNT) ct.c[C_PHOTON] += count;
       for (int q = 0; q < count; ++q) {
         const double* ph = S.ppos + 3 * (size_t)(start + q);
@@ -1211,13 +1211,13 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
 #pragma unroll
       for (int side = 0; side < 2; ++side) {
         const int32_t c = side ? nd.right : nd.left;
-        const int cnt = side ? nd.pad[3] : nd.pad[1];
+        const int cnt = side ? nd.padR[0] : nd.pad[1];
         const double* mn = side ? nd.rmin : nd.lmin;
         const double* mx = side ? nd.rmax : nd.lmax;
         if (c >= 0 && cnt >= K && nxt < 0 && box_d2(mn, mx, pos) == 0.0) nxt = c;
       }
       if (nxt < 0) {
-        if (nd.pad[4] >= K) {
+        if (nd.padR[1] >= K) {
           double mn[3], mx[3], e[3], f[3];
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
@@ -1230,7 +1230,7 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
           R2far = fmin(R2max, far2 * (1 + 0x1p-40));
           // photons lie on surfaces: density over the box's two largest extents
           const double a = fmax(fmax(e[0] * e[1], e[0] * e[2]), e[1] * e[2]);
-          R2dens = fmin(R2far, 1.3 * K * a / (PI_D * nd.pad[4]));
+          R2dens = fmin(R2far, 1.3 * K * a / (PI_D * nd.padR[1]));
         }
         break;
       }

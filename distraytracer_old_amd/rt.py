@@ -263,6 +263,26 @@ class Scene:
         self.close()
 
 
+# NodeD (csrc/rt_types.h): one 64-B line per child
+NODE_DTYPE = np.dtype([("lmin", "<f8", 3), ("lmax", "<f8", 3), ("left", "<i4"), ("pad", "<i4", 3),
+                       ("rmin", "<f8", 3), ("rmax", "<f8", 3), ("right", "<i4"), ("padR", "<i4", 3)])
+assert NODE_DTYPE.itemsize == 128
+
+
+def photon_maps_equal(a, b) -> bool:
+    """Two Scene.photon_map() results are the same structure: refs / ranges / counts and the
+    leaf-ordered photons bit-equal, boxes equal as numbers (a zero bound may carry either sign)."""
+    na, ra, pa, wa = a
+    nb, rb, pb, wb = b
+    if na.shape != nb.shape or ra != rb:
+        return False
+    x, y = na.view(NODE_DTYPE).ravel(), nb.view(NODE_DTYPE).ravel()
+    ints = all(np.array_equal(x[f], y[f]) for f in ("left", "pad", "right", "padR"))
+    boxes = all(np.array_equal(x[f], y[f]) for f in ("lmin", "lmax", "rmin", "rmax"))
+    return ints and boxes and np.array_equal(pa.view(np.uint64), pb.view(np.uint64)) and \
+        np.array_equal(wa.view(np.uint64), wb.view(np.uint64))
+
+
 def argb_to_rgb8(argb: np.ndarray) -> np.ndarray:
     a = argb.view(np.uint32)
     return np.stack([(a >> 16) & 255, (a >> 8) & 255, a & 255], -1).astype(np.uint8)

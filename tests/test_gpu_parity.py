@@ -224,15 +224,7 @@ def test_tile_schedule_does_not_change_the_image():
 
 
 def _maps_equal(a, b):
-    """Two photon maps (Scene.photon_map()) are the same structure: node refs / ranges / counts
-    bit-equal, boxes equal as numbers (a box bound's zero may carry either sign), leaf-ordered
-    photons bit-equal."""
-    na, ra, pa, wa = a
-    nb, rb, pb, wb = b
-    assert na.shape == nb.shape and ra == rb
-    assert np.array_equal(na[:, 96:], nb[:, 96:])  # left, right, pad[6]
-    assert np.array_equal(na[:, :96].view(np.float64), nb[:, :96].view(np.float64))
-    assert np.array_equal(pa.view(np.uint64), pb.view(np.uint64)) and np.array_equal(wa.view(np.uint64), wb.view(np.uint64))
+    assert rt.photon_maps_equal(a, b)
 
 
 def test_gpu_photon_map_build_equals_host_build(tmp_path, monkeypatch):

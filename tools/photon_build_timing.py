@@ -31,11 +31,7 @@ def timed_set(cli, pos, pwr, mode):
 
 
 def same(a, b):
-    na, ra, pa, wa = a
-    nb, rb, pb, wb = b
-    return (na.shape == nb.shape and ra == rb and np.array_equal(na[:, 96:], nb[:, 96:])
-            and np.array_equal(na[:, :96].view(np.float64), nb[:, :96].view(np.float64))
-            and np.array_equal(pa, pb) and np.array_equal(wa, wb))
+    return rt.photon_maps_equal(a, b)
 
 
 def main():
