@@ -105,6 +105,17 @@ DEVI TriG sload_tri(const TriD* t) {
   g.dB = sload(&t->dB);
   return g;
 }
+DEVI void sload_inv(const XformD* x, double* m) {  // rows 0..2 of a CTM inverse (all multVert reads)
+#pragma unroll
+  for (int i = 0; i < 12; ++i) m[i] = sload(x->inv + i);
+}
+DEVI AccelD sload_accel(const AccelD* p) {
+  AccelD a;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) { a.bmin[c] = sload(p->bmin + c); a.bmax[c] = sload(p->bmax + c); }
+  a.xf = sload(&p->xf); a.root = sload(&p->root); a.is_list = sload(&p->is_list); a.pad = 0;
+  return a;
+}
 DEVI TopD sload_top(const TopD* p) {
   TopD t;
   t.kind = sload(&p->kind); t.idx = sload(&p->idx); t.xf = sload(&p->xf); t.key = sload(&p->key);
@@ -488,10 +499,17 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       inst_closest<CNT, F>(S, tp.idx, w, k, i, best, local, ct);
       continue;
     }
-    const double* inv = S.xf[tp.xf].inv;
-    V o = xpt(inv, w.o), d = xvec(inv, w.d);
+    V o, d;
+    if (PK) {  // wave-uniform records: scalar loads
+      double inv[12];
+      sload_inv(S.xf + tp.xf, inv);
+      o = xpt(inv, w.o); d = xvec(inv, w.d);
+    } else {
+      const double* inv = S.xf[tp.xf].inv;
+      o = xpt(inv, w.o); d = xvec(inv, w.d);
+    }
     if (tp.kind == TOP_ACCEL) {
-      const AccelD& A = S.accel[tp.idx];
+      const AccelD A = PK ? sload_accel(S.accel + tp.idx) : S.accel[tp.idx];
       if (CNT) { ct.c[C_ROOT]++; ct.c[C_BOX]++; }
       RayInv ri = ray_inv(o, d, S.fastSlab);
       if (!box_hit(A.bmin, A.bmax, o, d, ri)) continue;
@@ -503,7 +521,7 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
       int args;
-      if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, LimClosest{best.t, best.t}) && t < best.t) {
+      if (test_ref_u<CNT, F, PK>(S, ref, o, d, k, t, args, ct, LimClosest{best.t, best.t}) && t < best.t) {
         best.t = t; best.ref = ref; best.top = (int16_t)i; best.inAcc = 0; best.ver = w.ver; best.inst = -1; best.iver = 0;
       }
     }
@@ -657,19 +675,26 @@ DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters
       if (inst_any<CNT, F>(S, tp.idx, w, k, dist, ct)) return true;
       continue;
     }
-    const double* inv = S.xf[tp.xf].inv;
-    V o = xpt(inv, w.o), d = xvec(inv, w.d);
+    V o, d;
+    if (PK) {  // wave-uniform records: scalar loads
+      double inv[12];
+      sload_inv(S.xf + tp.xf, inv);
+      o = xpt(inv, w.o); d = xvec(inv, w.d);
+    } else {
+      const double* inv = S.xf[tp.xf].inv;
+      o = xpt(inv, w.o); d = xvec(inv, w.d);
+    }
     if (tp.kind == TOP_ACCEL) {
       if (CNT) ct.c[C_ROOT]++;
       w.moved = false;
-      if (PK ? accel_any_pk<CNT, F>(S, S.accel[tp.idx], o, d, w, k, dist, ct)
+      if (PK ? accel_any_pk<CNT, F>(S, sload_accel(S.accel + tp.idx), o, d, w, k, dist, ct)
              : accel_any<CNT, F, false>(S, S.accel[tp.idx], o, d, w, k, dist, ct))
         return true;
     } else {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
       int args;
-      if (test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, LimShadow{dist}) && (dist - t) > EPS) return true;
+      if (test_ref_u<CNT, F, PK>(S, ref, o, d, k, t, args, ct, LimShadow{dist}) && (dist - t) > EPS) return true;
     }
   }
   return false;
@@ -1379,9 +1404,16 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
   double r = 0, g = 0, b = 0;
   for (int li = 0; li < S.nlight; ++li) {
     const LightD& L = S.light[li];
-    const bool disk = (F & FT_LIGHTX) && L.type == 2;
-    V lo = disk ? disk_pos(L, k, 0) : ld3(L.origin);
-    V ln = xpt(L.g, lo);
+    // li is wave-uniform: the light record's hot fields are scalar loads
+    const int32_t ltype = sload(&L.type);
+    double lg[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) lg[q] = sload(L.g + q);
+    const V lorg = mk(sload(L.origin), sload(L.origin + 1), sload(L.origin + 2));
+    const V lcol = mk(sload(L.color), sload(L.color + 1), sload(L.color + 2));
+    const bool disk = (F & FT_LIGHTX) && ltype == 2;
+    V lo = disk ? disk_pos(L, k, 0) : lorg;
+    V ln = xpt(lg, lo);
     ln = nrmz(mk(ln.x - h.fwd.x, ln.y - h.fwd.y, ln.z - h.fwd.z));
     WRay sr;
     sr.o = h.fwd;
@@ -1390,11 +1422,11 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     sr.stable = false;
     sr.moved = false;
     sr.ver = 0;
-    V lo2 = disk ? disk_pos(L, k, 2) : ld3(L.origin);
+    V lo2 = disk ? disk_pos(L, k, 2) : lorg;
     double t = sqrt((((sr.o.x - lo2.x) * (sr.o.x - lo2.x)) + ((sr.o.y - lo2.y) * (sr.o.y - lo2.y))) + ((sr.o.z - lo2.z) * (sr.o.z - lo2.z)));
     double ltMult = 1;
     if (CNT) ct.c[C_LIGHT]++;
-    if ((F & FT_LIGHTX) && L.type == 1) {  // mySpotLight.intersectCheck / calcT_Mult (myLight.java:77-82,159-163)
+    if ((F & FT_LIGHTX) && ltype == 1) {  // mySpotLight.intersectCheck / calcT_Mult (myLight.java:77-82,159-163)
       double angle = acos(-1 * dot(sr.d, ld3(L.orient)));
       ltMult = (angle < L.innerRad) ? 1 : (angle > L.outerRad) ? 0 : (L.outerRad - angle) / L.radDiff;
     }
@@ -1409,9 +1441,9 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     renorm(sr);  // shadowRay.direction._normalize()
     double ldp = dot(sr.d, h.nrm) * ltMult;
     if (ldp > EPS) {
-      r += tex.x * L.color[0] * ldp;
-      g += tex.y * L.color[1] * ldp;
-      b += tex.z * L.color[2] * ldp;
+      r += tex.x * lcol.x * ldp;
+      g += tex.y * lcol.y * ldp;
+      b += tex.z * lcol.z * ldp;
     }
 #ifdef RT_PROF_NOPHONG  // profiling builds only: results differ
     continue;
@@ -1425,9 +1457,9 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     double hdp = (hv.x * hr * h.nrm.x + hv.y * hr * h.nrm.y + hv.z * hr * h.nrm.z) * ltMult;
     if (hdp > EPS) {
       double ph = pow_shade(hdp * hdp, m.phong);
-      r += m.specular[0] * L.color[0] * ph;
-      g += m.specular[1] * L.color[1] * ph;
-      b += m.specular[2] * L.color[2] * ph;
+      r += m.specular[0] * lcol.x * ph;
+      g += m.specular[1] * lcol.y * ph;
+      b += m.specular[2] * lcol.z * ph;
     }
   }
   return mk(r, g, b);
