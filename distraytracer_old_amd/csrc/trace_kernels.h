@@ -736,8 +736,15 @@ DEVI HitRec make_hit(const SceneD& S, const Best& b, const WRay& w, const Key& k
   V tro = direct ? ro : xpt(X.inv, ro), trd = direct ? dw : xvec(X.inv, dw);
   double t = b.t, tt;
   int args = 0;
-  Counters dummy;
-  test_ref<false, F>(S, ref, tro, trd, k, tt, args, dummy);  // recompute args (deterministic)
+  if (!(F & FT_PRIM) || ref >= 0) {
+    // a triangle's only hit argument is its orientation: planar_test's st = (nA . d > 0), the
+    // same product of the same operands as in the winning test
+    const V nA = ld3(S.tri[ref].n);
+    args = dot(nA, trd) > 0 ? 1 : 0;
+  } else {
+    Counters dummy;
+    test_ref<false, F>(S, ref, tro, trd, k, tt, args, dummy);  // recompute args (deterministic)
+  }
   h.args = args;
   V p = mk(trd.x * t + tro.x, trd.y * t + tro.y, trd.z * t + tro.z);
   h.hitLoc = p;
