@@ -1213,6 +1213,67 @@ DEVI void photon_scan(const SceneD& S, const double* pos, double R2, Counters& c
   }
 }
 
+// photon_scan as a packet traversal (render kernel): the lanes shading nearby points of
+// one pixel tile walk ONE photon-BVH node sequence -- the union of their own scans, in the
+// same depth-first order (push left / right child, pop last-in first) -- with node
+// records and leaf photons as scalar loads; a lane tests a child box, or a leaf's photons,
+// only where its own scan would (lane mask per frame). Every lane therefore calls f with the
+// same photons in the same order as photon_scan (results bit-identical) while each photon
+// record is read once per wave instead of once per lane.
+template <bool CNT, class Fn>
+DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f) {
+  lds_i32* fN = pkN();  // the ray traversal's wave-uniform frames (idle during shading)
+  lds_u64* fM = pkM();
+  int sp = 0;
+  int32_t N = S.photonRoot;
+  uint64_t act = __ballot(1);
+  while (true) {
+    if (CNT && in_mask(act)) ct.c[C_PHOTON]++;
+    const NodeD* nd = S.pnode + N;
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const ChildBox cb = sload_child(nd, side);
+      bool in = false;
+      if (in_mask(act)) in = box_d2(cb.mn, cb.mx, pos) < R2;
+      const uint64_t m = __ballot(in);
+      if (!m) continue;
+      if (cb.ref >= 0) {
+        fN[sp] = cb.ref;
+        fM[sp] = m;
+        sp++;
+        continue;
+      }
+      const int start = sload(side ? &nd->pad[2] : &nd->pad[0]), count = sload(side ? &nd->padR[0] : &nd->pad[1]);
+      if (CNT && in_mask(m)) ct.c[C_PHOTON] += count;
+      for (int q0 = 0; q0 < count; q0 += 4) {  // 4 photons' positions per scalar-load batch
+        double px[4], py[4], pz[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (q0 + j < count) {
+            const double* ph = S.ppos + 3 * (size_t)(start + q0 + j);
+            px[j] = sload(ph); py[j] = sload(ph + 1); pz[j] = sload(ph + 2);
+          }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (q0 + j < count && in_mask(m)) {
+            const double dx = pos[0] - px[j], dy = pos[1] - py[j], dz = pos[2] - pz[j];
+            const double d2 = dx * dx + dy * dy + dz * dz;  // as photon_scan
+            if (d2 < R2) f(d2, start + q0 + j);
+          }
+      }
+    }
+    if (sp == 0) break;
+    --sp;
+    N = uni(fN[sp]);
+    act = uni64(fM[sp]);
+  }
+}
+template <bool CNT, class Fn>
+DEVI void photon_scan_any(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f) {
+  if (PACKET) photon_scan_pk<CNT>(S, pos, R2, ct, f);
+  else photon_scan<CNT>(S, pos, R2, ct, f);
+}
+
 // The k nearest photons by selection instead of a heap (no per-lane memory): the
 // k-th smallest d^2 is bracketed by counting passes -- 8 cumulative counters against
 // edges e_1..e_8 of the current window [lo, hi) -- until the window holding the k-th
@@ -1280,7 +1341,7 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
     for (int k = 0; k < 7; ++k) e[k] = lo + (k + 1) * w;
     e[7] = hi;
     uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // photons with d2 < e[k] (including the `below` ones)
-    photon_scan<CNT>(S, pos, hi, ct, [&](double d2, int) {
+    photon_scan_any<CNT>(S, pos, hi, ct, [&](double d2, int) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) c[k] += (d2 < e[k]) ? 1u : 0u;
     });
@@ -1303,7 +1364,7 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
   V res = mk(0, 0, 0);
   double rSq = 0;
   int n = 0;
-  photon_scan<CNT>(S, pos, all ? R2max : hi, ct, [&](double d2, int i) {
+  photon_scan_any<CNT>(S, pos, all ? R2max : hi, ct, [&](double d2, int i) {
     if (all || d2 < lo) {
       const double* w = S.ppwr + 3 * (size_t)i;
       res.x += w[0]; res.y += w[1]; res.z += w[2];
