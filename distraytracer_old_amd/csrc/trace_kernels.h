@@ -1220,6 +1220,10 @@ DEVI void photon_scan(const SceneD& S, const double* pos, double R2, Counters& c
 // only where its own scan would (lane mask per frame). Every lane therefore calls f with the
 // same photons in the same order as photon_scan (results bit-identical) while each photon
 // record is read once per wave instead of once per lane.
+#ifndef RT_PH_BATCH
+#define RT_PH_BATCH 1
+#endif
+static constexpr int PH_BATCH = RT_PH_BATCH;
 template <bool CNT, class Fn>
 DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f) {
   lds_i32* fN = pkN();  // the ray traversal's wave-uniform frames (idle during shading)
@@ -1245,16 +1249,16 @@ DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters
       }
       const int start = sload(side ? &nd->pad[2] : &nd->pad[0]), count = sload(side ? &nd->padR[0] : &nd->pad[1]);
       if (CNT && in_mask(m)) ct.c[C_PHOTON] += count;
-      for (int q0 = 0; q0 < count; q0 += 4) {  // 4 photons' positions per scalar-load batch
-        double px[4], py[4], pz[4];
+      for (int q0 = 0; q0 < count; q0 += PH_BATCH) {  // PH_BATCH photons' positions per scalar-load batch
+        double px[PH_BATCH], py[PH_BATCH], pz[PH_BATCH];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < PH_BATCH; ++j)
           if (q0 + j < count) {
             const double* ph = S.ppos + 3 * (size_t)(start + q0 + j);
             px[j] = sload(ph); py[j] = sload(ph + 1); pz[j] = sload(ph + 2);
           }
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < PH_BATCH; ++j)
           if (q0 + j < count && in_mask(m)) {
             const double dx = pos[0] - px[j], dy = pos[1] - py[j], dz = pos[2] - pz[j];
             const double d2 = dx * dx + dy * dy + dz * dz;  // as photon_scan
