@@ -96,9 +96,24 @@ class FrameExchange:
         tile = self.tiles[self.frame % 2]
         render(tile)  # enqueued before the previous frame's gather is waited for: they overlap
         self._complete()  # frame-1 gathered + assembled; its tile buffer is free again
-        outs = list(self.gathered.unbind(0)) if self.rank == 0 else None
-        self._pending = self.dist.gather(tile, outs, dst=0, async_op=True)
+        self._pending = self._gather(tile)
         self.frame += 1
+
+    def _gather(self, tile):
+        if not getattr(self, "_use_allgather", False):
+            try:
+                outs = list(self.gathered.unbind(0)) if self.rank == 0 else None
+                return self.dist.gather(tile, outs, dst=0, async_op=True)
+            except (RuntimeError, ValueError, NotImplementedError):
+                # a backend without gather: the same exchange as an all-gather (every rank
+                # receives every tile; only rank 0 assembles them)
+                self._use_allgather = True
+        if getattr(self, "_ag", None) is None:
+            import torch
+            self._ag = torch.empty((self.world,) + tuple(tile.shape), dtype=tile.dtype, device=tile.device)
+            if self.rank == 0:
+                self.gathered = self._ag
+        return self.dist.all_gather_into_tensor(self._ag.view(-1), tile.view(-1), async_op=True)
 
     def finish(self):
         self._complete()

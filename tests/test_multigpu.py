@@ -6,6 +6,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -69,7 +70,7 @@ def test_gloo_world2_gather_equals_single_image():
     assert np.array_equal(full, ref)
 
 
-def _exchange_worker(rank, world, port, H, W, q):
+def _exchange_worker(rank, world, port, H, W, q, allgather=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -77,6 +78,7 @@ def _exchange_worker(rank, world, port, H, W, q):
     rows = torch.tensor(multigpu.image_rows(rank, world, H, band), dtype=torch.float32)
     maxrows = multigpu.max_tile_rows(world, H, band)
     ex = multigpu.FrameExchange(dist, H, (maxrows, W, 1), "cpu", band=band)
+    ex._use_allgather = allgather  # the fallback for backends without gather
     seen = []
     for f in range(4):
         def render(tile, f=f):  # frame f's pixel value: 1000 * f + image row
@@ -95,14 +97,16 @@ def _exchange_worker(rank, world, port, H, W, q):
     dist.destroy_process_group()
 
 
-def test_gloo_world3_pipelined_exchange_delivers_every_frame():
+@pytest.mark.parametrize("allgather", [False, True])
+def test_gloo_world3_pipelined_exchange_delivers_every_frame(allgather):
     """FrameExchange (bench.py's N-GPU step): frame i's gather overlaps frame i+1's render;
-    rank 0 still assembles every frame exactly, and finish() drains the last one."""
+    rank 0 still assembles every frame exactly, and finish() drains the last one (also through
+    the all-gather fallback)."""
     H, W, world = 13, 3, 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_exchange_worker, args=(r, world, port, H, W, q)) for r in range(world)]
+    ps = [ctx.Process(target=_exchange_worker, args=(r, world, port, H, W, q, allgather)) for r in range(world)]
     for p in ps:
         p.start()
     frames = q.get(timeout=120)
