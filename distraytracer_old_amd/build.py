@@ -42,7 +42,9 @@ def build(force: bool = False, verbose: bool = False, defines: list[str] | None 
     for src in SOURCES:  # .hip -> device+host; .cpp -> host-only C++ (no device pass)
         obj = target.parent / (tag + src + ".o")
         lang = [] if src.endswith(".hip") else ["-x", "c++"]
-        cmd = [HIPCC, *COMPILE_FLAGS, *["-D" + d for d in (defines or [])], *lang, "-c", str(CSRC / src), "-o", str(obj)]
+        # defines starting with "-" are extra compiler flags (tuning experiments)
+        dflags = [d if d.startswith("-") else "-D" + d for d in (defines or [])]
+        cmd = [HIPCC, *COMPILE_FLAGS, *dflags, *lang, "-c", str(CSRC / src), "-o", str(obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         logs.append(r.stderr)
         if r.returncode != 0:

@@ -28,6 +28,9 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "nophong": ["RT_PROF_NOPHONG"],
     "noshade": ["RT_PROF_NOSHADE"],            # camera rays traced, no hit record / shading
     "notrace": ["RT_PROF_NOTRACE"],            # camera rays generated, nothing traced
+    "wprio": ["-Xarch_device", "-mllvm=--amdgpu-set-wave-priority"],  # compiler flags (results equal)
+    "itsched": ["-Xarch_device", "-mllvm=--amdgpu-sched-strategy=gcn-iterative-max-occupancy-experimental"],
+    "bias0": ["-Xarch_device", "-mllvm=--amdgpu-schedule-metric-bias=0"],
     "tl": ["RT_PROF_TIMELINE"],               # workgroup timeline (tools/timeline.py)
     "pkstat": ["RT_PROF_PKSTAT"],             # packet lane utilisation (tools/pkstat.py)
 }
