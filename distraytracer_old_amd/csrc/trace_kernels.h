@@ -1279,8 +1279,8 @@ DEVI void photon_scan_any(const SceneD& S, const double* pos, double R2, Counter
 }
 
 // The k nearest photons by selection instead of a heap (no per-lane memory): the
-// k-th smallest d^2 is bracketed by counting passes -- 8 cumulative counters against
-// edges e_1..e_8 of the current window [lo, hi) -- until the window holding the k-th
+// k-th smallest d^2 is bracketed by counting passes -- KNN_EDGES (16) cumulative counters
+// against equally spaced edges of the current window [lo, hi) -- until the window holding the k-th
 // photon has <= KNN_SHELL photons; a last pass sums every photon below the window and
 // the nearest (k - below) window photons (kept sorted in registers). Same k-set and
 // largest d^2 as the heap; the powers are summed in scan order rather than the
@@ -1288,7 +1288,14 @@ DEVI void photon_scan_any(const SceneD& S, const double* pos, double R2, Counter
 // Start window: [0, R2) with R2 from the local density of the smallest photon-BVH node
 // around p holding >= k photons; if fewer than k photons fall below it, the next try is
 // that node's far-corner distance (all its photons lie within it), then max_dist^2.
-static constexpr int KNN_SHELL = 8;
+#ifndef RT_KNN_SHELL
+#define RT_KNN_SHELL 8
+#endif
+#ifndef RT_KNN_EDGES
+#define RT_KNN_EDGES 16
+#endif
+static constexpr int KNN_SHELL = RT_KNN_SHELL;
+static constexpr int KNN_EDGES = RT_KNN_EDGES;  // counters per counting pass
 template <bool CNT>
 DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
 #ifdef RT_KNN_HEAP
@@ -1339,26 +1346,39 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
   int below = 0;
   bool all = false;  // fewer than K photons within max_dist: the set is all of them
   for (int level = 0; level < 32; ++level) {
-    double e[8];
-    const double w = (hi - lo) * 0.125;
+    constexpr int NE = KNN_EDGES;
+    double e[NE];
+    const double w = (hi - lo) * (1.0 / NE);
 #pragma unroll
-    for (int k = 0; k < 7; ++k) e[k] = lo + (k + 1) * w;
-    e[7] = hi;
-    uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // photons with d2 < e[k] (including the `below` ones)
+    for (int k = 0; k < NE - 1; ++k) e[k] = lo + (k + 1) * w;
+    e[NE - 1] = hi;
+    uint32_t c[NE];  // photons with d2 < e[k] (including the `below` ones)
+#pragma unroll
+    for (int k = 0; k < NE; ++k) c[k] = 0;
     photon_scan_any<CNT>(S, pos, hi, ct, [&](double d2, int) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) c[k] += (d2 < e[k]) ? 1u : 0u;
+      for (int k = 0; k < NE; ++k) c[k] += (d2 < e[k]) ? 1u : 0u;
     });
-    if ((int)c[7] < K) {  // only possible for the start window: widen it
+    if ((int)c[NE - 1] < K) {  // only possible for the start window: widen it
       if (hi == R2max) { all = true; break; }
       hi = (hi < R2far) ? R2far : R2max;
       continue;
     }
-    int b = 0;
-    while ((int)c[b] < K) ++b;  // first edge with >= K photons below it
-    if (b) { lo = e[b - 1]; below = (int)c[b - 1]; }
-    hi = e[b];
-    if ((int)c[b] - below <= KNN_SHELL || !(lo < hi)) break;
+    // first edge b with >= K photons below it (selects, no dynamic register indexing)
+    double nlo = lo, nhi = hi;
+    int nbelow = below, cb = (int)c[NE - 1];
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      if (!found && (int)c[k] >= K) {
+        found = true;
+        nhi = e[k];
+        cb = (int)c[k];
+        if (k) { nlo = e[k - 1]; nbelow = (int)c[k - 1]; }
+      }
+    }
+    lo = nlo; hi = nhi; below = nbelow;
+    if (cb - below <= KNN_SHELL || !(lo < hi)) break;
   }
   // --- final pass: every photon below the window, and the nearest K - below window photons
   double sd[KNN_SHELL];

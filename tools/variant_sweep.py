@@ -31,6 +31,10 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "wprio": ["-Xarch_device", "-mllvm=--amdgpu-set-wave-priority"],  # compiler flags (results equal)
     "itsched": ["-Xarch_device", "-mllvm=--amdgpu-sched-strategy=gcn-iterative-max-occupancy-experimental"],
     "bias0": ["-Xarch_device", "-mllvm=--amdgpu-schedule-metric-bias=0"],
+    "ed8": [],
+    "ed16": ["RT_KNN_EDGES=16"],
+    "ed32": ["RT_KNN_EDGES=32"],
+    "ed16sh12": ["RT_KNN_EDGES=16", "RT_KNN_SHELL=12"],
     "tl": ["RT_PROF_TIMELINE"],               # workgroup timeline (tools/timeline.py)
     "pkstat": ["RT_PROF_PKSTAT"],             # packet lane utilisation (tools/pkstat.py)
 }
