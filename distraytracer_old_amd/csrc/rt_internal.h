@@ -70,6 +70,7 @@ struct rt_scene {
   size_t devBytes = 0;
   bool photonsUploaded = false;
   void* counters = nullptr;  // device uint64[RT_ST_N]
+  const double* noCullBound = nullptr;  // device [ntop][4] of -1 (RT_RENDER_NOCULL)
   // tile schedules (longest tiles first) per tile layout (trace.hip `schedule`)
   struct TileSchedule {
     std::string key;

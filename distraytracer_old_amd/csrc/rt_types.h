@@ -138,6 +138,8 @@ struct SceneD {
   const int32_t* member;
   const AccelD* accel;
   const TopD* top;
+  const double* topBound;  // [ntop][4]: world bounding sphere (centre, radius) of a top-level
+                           // implicit primitive, radius < 0 = none (trace.hip top_bounds)
   const MatD* mat;
   const LightD* light;
   const TexD* tex;

@@ -52,6 +52,65 @@ static int upload(rt_scene* s, const std::vector<T>& v, const T** out) {
   return RT_OK;
 }
 
+// Conservative world-space bounding spheres of the top-level implicit primitives (spheres,
+// moving spheres, capped / hollow cylinders, rendered boxes): the object-space box of the
+// shape (a cylinder's y range widened by its 1e-7 acceptance slack), its 8 corners through
+// the CTM, the sphere around their box, inflated by 1e-6 relative + absolute. A ray that
+// misses it, or enters it beyond the current best hit / the shadow distance, cannot produce
+// a hit the reference would keep (closest / any-hit) -- see closest() / shadowed().
+static std::vector<double> top_bounds(const HostScene& h) {
+  std::vector<double> b(4 * h.top.size(), -1.0);
+  for (size_t i = 0; i < h.top.size(); ++i) {
+    const TopD& t = h.top[i];
+    if (t.kind != TOP_PRIM) continue;
+    const PrimD& P = h.prim[t.idx];
+    double mn[3], mx[3];
+    switch (P.type) {
+      case PT_SPHERE:
+      case PT_MSPHERE:
+        for (int c = 0; c < 3; ++c) {
+          const double r = std::fabs(P.a[3 + c]);
+          mn[c] = P.a[c] - r; mx[c] = P.a[c] + r;
+          if (P.type == PT_MSPHERE) { mn[c] = std::min(mn[c], P.a[6 + c] - r); mx[c] = std::max(mx[c], P.a[6 + c] + r); }
+        }
+        break;
+      case PT_CYL:
+      case PT_HCYL: {
+        const double rx = std::fabs(P.a[3]), rz = std::fabs(P.a[4]);
+        mn[0] = P.a[0] - rx; mx[0] = P.a[0] + rx;
+        mn[2] = P.a[2] - rz; mx[2] = P.a[2] + rz;
+        mn[1] = std::min(P.a[7], P.a[6]) - 1e-6; mx[1] = std::max(P.a[7], P.a[6]) + 1e-6;
+        break;
+      }
+      case PT_BOX:
+        for (int c = 0; c < 3; ++c) { mn[c] = P.a[c]; mx[c] = P.a[3 + c]; }
+        break;
+      default:
+        continue;  // quads / planes / instances: never culled
+    }
+    const double* g = h.xf[t.xf].g;
+    double wmn[3] = {1e300, 1e300, 1e300}, wmx[3] = {-1e300, -1e300, -1e300};
+    for (int k = 0; k < 8; ++k) {
+      const double p[3] = {(k & 1) ? mx[0] : mn[0], (k & 2) ? mx[1] : mn[1], (k & 4) ? mx[2] : mn[2]};
+      for (int r = 0; r < 3; ++r) {
+        const double w = g[r * 4 + 0] * p[0] + g[r * 4 + 1] * p[1] + g[r * 4 + 2] * p[2] + g[r * 4 + 3];
+        wmn[r] = std::min(wmn[r], w); wmx[r] = std::max(wmx[r], w);
+      }
+    }
+    double c[3], hd2 = 0, cn = 0;
+    for (int r = 0; r < 3; ++r) {
+      c[r] = 0.5 * (wmn[r] + wmx[r]);
+      const double e = 0.5 * (wmx[r] - wmn[r]);
+      hd2 += e * e;
+      cn += c[r] * c[r];
+    }
+    const double R = std::sqrt(hd2) * (1 + 1e-6) + 1e-6 * (1 + std::sqrt(cn));
+    if (!std::isfinite(R) || !std::isfinite(cn)) continue;
+    b[4 * i + 0] = c[0]; b[4 * i + 1] = c[1]; b[4 * i + 2] = c[2]; b[4 * i + 3] = R;
+  }
+  return b;
+}
+
 static int upload_scene(rt_scene* s) {
   HostScene& h = s->hs;
   SceneD& d = s->dev;
@@ -68,6 +127,10 @@ static int upload_scene(rt_scene* s) {
     if (need && (rc = upload(s, h.triUV, &d.triUV))) return rc;
   }
   d.ntop = (int)h.top.size();
+  {
+    const std::vector<double> tb = top_bounds(h), none(tb.size(), -1.0);
+    if ((rc = upload(s, tb, &d.topBound)) || (rc = upload(s, none, &s->noCullBound))) return rc;
+  }
   d.nlight = (int)h.light.size();
   d.pnode = nullptr;
   d.ppos = d.ppwr = nullptr;
@@ -365,12 +428,14 @@ static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, 
 #endif
   int tilesX = (P.W + P.tw - 1) / P.tw, tilesY = (P.nrows + P.th - 1) / P.th;
   dim3 grid(dv::xcd_grid(tilesX * tilesY)), block(64);
+  SceneD sd = s->dev;
+  if (flags & RT_RENDER_NOCULL) sd.topBound = s->noCullBound;
   if (count) {  // counting always runs the all-features kernel
     HIPCHK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long) * RT_ST_N, st));
-    hipLaunchKernelGGL((dv::render_kernel<true, dv::FT_ALL>), grid, block, dv::LDS_BYTES, st, s->dev, P, d_rgb, d_argb,
+    hipLaunchKernelGGL((dv::render_kernel<true, dv::FT_ALL>), grid, block, dv::LDS_BYTES, st, sd, P, d_rgb, d_argb,
                        (unsigned long long*)s->counters);
   } else {
-    hipLaunchKernelGGL(pick_variant(s->hs, flags), grid, block, dv::LDS_BYTES, st, s->dev, P, d_rgb, d_argb,
+    hipLaunchKernelGGL(pick_variant(s->hs, flags), grid, block, dv::LDS_BYTES, st, sd, P, d_rgb, d_argb,
                        (unsigned long long*)nullptr);
   }
   HIPCHK(hipGetLastError());

@@ -481,6 +481,27 @@ DEVI void inst_closest(const SceneD& S, int32_t ii, WRay& w, const Key& k, int t
   }
 }
 
+// Top-level culling of implicit primitives by their world bounding sphere (trace.hip
+// top_bounds, inflated 1e-6): true when the world ray (w.o, w.d, |w.d| = 1 after renorm)
+// misses the sphere or enters it beyond `lim` (the running best hit / the shadow distance),
+// so the primitive's own test could not produce a hit the reference keeps. Its sphere
+// contains every point the test can accept by a margin far above the test's rounding, so
+// the outcome is the reference's; the primitive's RNG draws are keyed, not a stream (Q23),
+// so skipping a test shifts nothing else.
+template <bool PK>
+DEVI bool top_culled(const SceneD& S, int i, const WRay& w, double lim) {
+  const double* b = S.topBound + 4 * i;
+  const double R = PK ? sload(b + 3) : b[3];
+  if (!(R > 0)) return false;
+  const V c = PK ? mk(sload(b), sload(b + 1), sload(b + 2)) : mk(b[0], b[1], b[2]);
+  const V oc = mk(c.x - w.o.x, c.y - w.o.y, c.z - w.o.z);
+  const double tca = dot(oc, w.d), oc2 = dot(oc, oc);
+  const double d2 = oc2 - tca * tca, R2 = R * R;
+  if (d2 - R2 > 1e-9 * (oc2 + R2)) return true;  // misses the sphere
+  const double tn = tca - sqrt(fmax(R2 - d2, 0.0));
+  return tn > lim + 1e-9 * (fabs(lim) + sqrt(oc2) + R);  // enters it beyond lim
+}
+
 // findClosestRayHit (myScene.java:888-903): objList scan, TreeMap keeps the first of equal t
 #ifndef RT_PACKET
 #define RT_PACKET 1
@@ -499,6 +520,7 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       inst_closest<CNT, F>(S, tp.idx, w, k, i, best, local, ct);
       continue;
     }
+    if ((F & FT_PRIM) && tp.kind == TOP_PRIM && top_culled<PK>(S, i, w, best.t)) continue;
     V o, d;
     if (PK) {  // wave-uniform records: scalar loads
       double inv[12];
@@ -675,6 +697,7 @@ DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters
       if (inst_any<CNT, F>(S, tp.idx, w, k, dist, ct)) return true;
       continue;
     }
+    if ((F & FT_PRIM) && tp.kind == TOP_PRIM && top_culled<PK>(S, i, w, dist)) continue;
     V o, d;
     if (PK) {  // wave-uniform records: scalar loads
       double inv[12];

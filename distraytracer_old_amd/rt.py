@@ -137,6 +137,7 @@ def inspect_cli(cli: str, scene_dir=SCENE_DIR, textures: dict | None = None) -> 
 
 RENDER_GENERIC = 1  # RT_RENDER_GENERIC: the all-features kernel instead of the scene-specialised one
 RENDER_ROWMAJOR = 2  # RT_RENDER_ROWMAJOR: row-major tile dispatch instead of the longest-first schedule
+RENDER_NOCULL = 4  # RT_RENDER_NOCULL: no bounding-sphere culling of top-level primitives
 
 
 def params(W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, flags=0, row_band=1) -> RenderParams:

@@ -175,6 +175,8 @@ typedef struct rt_render_params {
 /* dispatch tiles in row-major order instead of the probed longest-first schedule
    (results are identical; for testing and timing the schedule) */
 #define RT_RENDER_ROWMAJOR 2u
+/* test every top-level primitive (no bounding-sphere culling): same image, slower */
+#define RT_RENDER_NOCULL 4u
 
 typedef struct rt_scene rt_scene;
 

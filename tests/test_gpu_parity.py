@@ -266,3 +266,14 @@ def test_gpu_photon_map_build_ties_and_sizes(tmp_path, monkeypatch, n):
         s.close()
     monkeypatch.delenv("DISTRAYTRACER_PHOTON_BUILD")
     _maps_equal(maps[0], maps[1])
+
+
+@pytest.mark.parametrize("cli,W,spp", [("plnts3ColsBunnies.cli", 128, 4), ("p2_t05.cli", 96, 2), ("c2clear.cli", 96, 1),
+                                       ("p2_t07.cli", 96, 2), ("c3shinyBall.cli", 96, 1)])
+def test_top_level_culling_does_not_change_the_image(cli, W, spp):
+    """Bounding-sphere culling of top-level spheres / cylinders / boxes (closest and any-hit)
+    renders bit-identically to testing every top-level primitive (RT_RENDER_NOCULL)."""
+    g = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+    a, aa = g.render(W, W, spp=spp, seed=SEED)
+    b, ab = g.render(W, W, spp=spp, seed=SEED, flags=rt.RENDER_NOCULL)
+    assert np.array_equal(aa, ab) and np.array_equal(a.view(np.uint32), b.view(np.uint32))
