@@ -57,6 +57,7 @@ static bool named_color(std::string n, Clr& c) {
 
 struct CliLoader {
   std::string dir, saveName;
+  int refine = -1;  // `refine on|off` (myScene.setRefine, myRTFileReader.java:111); -1 = not given
   std::map<std::string, int> texIndex;
   std::vector<Mat> stack{Mat::ident()};
   // material state
@@ -556,8 +557,12 @@ struct CliLoader {
           scale(num(t, 1), num(t, 2), num(t, 3));
         } else if (c == "rotate") {
           rotate(num(t, 1), num(t, 2), num(t, 3), num(t, 4));
-        } else if (c == "reset_timer" || c == "print_timer" || c == "refine") {
-          // timers and progressive `refine` are outside the kernel path (documented override)
+        } else if (c == "refine") {  // myScene.setRefine (myScene.java:796-803): progressive passes
+          std::string v = t.at(1);
+          for (auto& ch : v) ch = (char)std::tolower(ch);
+          refine = v == "on" ? 1 : 0;
+        } else if (c == "reset_timer" || c == "print_timer") {
+          // timers are outside the kernel path
         } else {
           err = "unsupported command '" + c + "' in " + fname;
           return false;
@@ -610,6 +615,7 @@ extern "C" int rt_scene_load_cli(const char* scene_dir, const char* cli_file, in
   if (rc) return rc;
   rc = rt_scene_create(&L.d, device, out);
   if (rc == RT_OK) (*out)->saveName = L.saveName.empty() ? std::string(cli_file) : L.saveName;
+  if (rc == RT_OK) (*out)->refine = L.refine == 1;
   return rc;
 }
 

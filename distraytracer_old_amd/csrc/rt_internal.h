@@ -64,6 +64,7 @@ int build_photon_tree_gpu(rt_scene* s, const double* pos, const double* pwr, int
 struct rt_scene {
   rt::HostScene hs;
   std::string saveName;  // `write` argument (or the .cli name) when loaded by rt_scene_load_cli
+  bool refine = false;   // `refine on` (rt_refine_steps / rt_render_pass)
   int device = 0;
   rt::SceneD dev{};
   std::vector<void*> allocs;

@@ -169,7 +169,7 @@ struct ParamsD {
   const int32_t* order;     // tile dispatch order (longest first), nullptr = row-major
   uint32_t* tcost;          // non-null: each wave writes its duration (s_memrealtime ticks) to tcost[tile]
   // camera (RT_CAMERA_*) with its per-image constants (setImageSize, myScene.java:780-792)
-  int32_t cam, pad2;
+  int32_t cam, colStep;  // colStep: every colStep-th column (a `refine` pass, rt_render_pass)
   double fishMult, xStart, yStart, aperHalf;  // fisheye
   double orthPerRow, orthPerCol;              // ortho
 };

@@ -289,7 +289,7 @@ static int make_params(rt_scene* s, const rt_render_params* p, ParamsD& P) {
   P.viewZ = -1 * (std::max(P.H, P.W) / 2.0) / std::tan(fovRad / 2);
   // myFishEyeScene / myOrthoScene constants (setImageSize :780-792, setSceneParams :1556-1560, :1683-1688)
   P.cam = s->hs.camera;
-  P.pad2 = 0;
+  P.colStep = 1;
   {
     const double maxDim = std::max(P.H, P.W), rayYOffset = P.H / 2.0, rayXOffset = P.W / 2.0;
     P.yStart = ((maxDim - P.H) / 2.0) - rayYOffset;
@@ -382,15 +382,16 @@ static int sort_tiles(rt_scene::TileSchedule& e, hipStream_t st) {
 static int schedule(rt_scene* s, ParamsD& P, bool count, hipStream_t st) {
   P.order = nullptr;
   P.tcost = nullptr;
-  if (P.nrows * (int64_t)P.W < (1 << 16)) return RT_OK;  // small renders: row-major
+  if (P.nrows * (int64_t)((P.W + P.colStep - 1) / P.colStep) < (1 << 16)) return RT_OK;  // small renders: row-major
   char key[160];
-  std::snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%.17g", P.W, P.H, P.row0, P.nrows, P.rowStep, P.band,
-                P.tw, P.th, P.G, P.viewZ);
+  std::snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%.17g", P.W, P.H, P.row0, P.nrows, P.rowStep, P.band,
+                P.colStep, P.tw, P.th, P.G, P.viewZ);
   rt_scene::TileSchedule* e = nullptr;
   for (auto& x : s->schedules)
     if (x.key == key) { e = &x; break; }
   if (!e) {
-    const int tilesX = (P.W + P.tw - 1) / P.tw, ntiles = tilesX * ((P.nrows + P.th - 1) / P.th);
+    const int ncols = (P.W + P.colStep - 1) / P.colStep;
+    const int tilesX = (ncols + P.tw - 1) / P.tw, ntiles = tilesX * ((P.nrows + P.th - 1) / P.th);
     uint32_t* d_cost = nullptr;
     int32_t* d_order = nullptr;
     HIPCHK(hipMalloc(&d_cost, sizeof(uint32_t) * ntiles));
@@ -426,7 +427,7 @@ static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, 
     if (rc) return rc;
   }
 #endif
-  int tilesX = (P.W + P.tw - 1) / P.tw, tilesY = (P.nrows + P.th - 1) / P.th;
+  int tilesX = ((P.W + P.colStep - 1) / P.colStep + P.tw - 1) / P.tw, tilesY = (P.nrows + P.th - 1) / P.th;
   dim3 grid(dv::xcd_grid(tilesX * tilesY)), block(64);
   SceneD sd = s->dev;
   if (flags & RT_RENDER_NOCULL) sd.topBound = s->noCullBound;
@@ -516,6 +517,72 @@ int rt_time_render(rt_scene* s, const rt_render_params* p, int warmup, int iters
   (void)hipFree(d_rgb);
   (void)hipFree(d_argb);
   return rc;
+}
+
+// myScene.setRefine (myScene.java:796-803): refIDX = (int)(log10(.5 (W + H) / 16) / log10 2),
+// steps pow2[refIDX], ..., pow2[0] (the image size is the render's, as for viewZ)
+int rt_refine_steps(const rt_scene* s, int width, int height, int* steps, int cap) {
+  if (!s || width <= 0 || height <= 0) return set_error(RT_E_INVALID, "rt_refine_steps: bad argument");
+  int n = 1;
+  int st[16] = {1};
+  if (s->refine) {
+    const int refIDX = (int)(std::log10(.5 * (width + height) / 16.0) / std::log10(2.0));
+    if (refIDX >= 0) {
+      n = std::min(refIDX, 15) + 1;
+      for (int i = n - 1; i >= 0; --i) st[n - 1 - i] = 1 << i;
+    }
+  }
+  for (int i = 0; i < n && i < cap && steps; ++i) steps[i] = st[i];
+  return n;
+}
+
+// One `refine` pass of myFOVScene.draw (myScene.java:1481-1531; fisheye / ortho / DOF alike):
+// the pixels (row, col) with row, col multiples of `step`, each written over its step x step
+// span (writePxlSpan, :1171-1177) in full-size host buffers; skip_origin leaves (0,0) alone
+// (`skipPxl`, every pass after the first). Pixel RNG keys are those of the full render, so
+// the last pass (step 1) reproduces rt_render everywhere but a skipped (0,0).
+int rt_render_pass(rt_scene* s, const rt_render_params* p, int step, int skip_origin, float* rgb, int32_t* argb) {
+  if (!s || !p || step <= 0) return set_error(RT_E_INVALID, "rt_render_pass: bad argument");
+  rt_render_params q = *p;
+  q.row0 = 0; q.row1 = p->height; q.row_step = step; q.row_band = 1;
+  ParamsD P;
+  int rc = make_params(s, &q, P);
+  if (rc) return rc;
+  P.colStep = step;
+  HIPCHK(hipSetDevice(s->device));
+  const int W = P.W, H = P.H, ncols = (W + step - 1) / step, nr = P.nrows;
+  const size_t npx = (size_t)nr * ncols;
+  float* d_rgb = nullptr;
+  int32_t* d_argb = nullptr;
+  HIPCHK(hipMalloc(&d_rgb, npx * 3 * sizeof(float)));
+  hipError_t e = hipMalloc(&d_argb, npx * sizeof(int32_t));
+  if (e != hipSuccess) { (void)hipFree(d_rgb); return set_error(RT_E_HIP, hipGetErrorString(e)); }
+  // a pass with step > 1 needs the column step (FT_PASS): the all-features kernel
+  rc = launch(s, P, step > 1 ? (p->flags | RT_RENDER_GENERIC) : p->flags, d_rgb, d_argb, false, 0);
+  std::vector<float> hr;
+  std::vector<int32_t> ha;
+  if (rc == RT_OK) {
+    e = hipDeviceSynchronize();
+    if (e == hipSuccess) { hr.resize(npx * 3); e = hipMemcpy(hr.data(), d_rgb, npx * 3 * sizeof(float), hipMemcpyDeviceToHost); }
+    if (e == hipSuccess) { ha.resize(npx); e = hipMemcpy(ha.data(), d_argb, npx * sizeof(int32_t), hipMemcpyDeviceToHost); }
+    if (e != hipSuccess) rc = set_error(RT_E_HIP, std::string("render pass: ") + hipGetErrorString(e));
+  }
+  (void)hipFree(d_rgb);
+  (void)hipFree(d_argb);
+  if (rc) return rc;
+  for (int r = 0; r < nr; ++r)
+    for (int c = 0; c < ncols; ++c) {
+      const int row = r * step, col = c * step;
+      if (skip_origin && row == 0 && col == 0) continue;
+      const size_t i = (size_t)r * ncols + c;
+      for (int y = row; y < std::min(row + step, H); ++y)
+        for (int x = col; x < std::min(col + step, W); ++x) {
+          const size_t o = (size_t)y * W + x;
+          if (argb) argb[o] = ha[i];
+          if (rgb) { rgb[3 * o] = hr[3 * i]; rgb[3 * o + 1] = hr[3 * i + 1]; rgb[3 * o + 2] = hr[3 * i + 2]; }
+        }
+    }
+  return RT_OK;
 }
 
 #ifdef RT_PROF_PKSTAT

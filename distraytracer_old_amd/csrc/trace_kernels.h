@@ -27,7 +27,8 @@ enum : uint32_t {
   FT_LIGHTX = 32, // spot or disk lights
   FT_CAMX = 64,   // fisheye or orthographic camera
   FT_INST = 128,  // instances (named_object / instance / sierpinski)
-  FT_ALL = 255
+  FT_PASS = 256,  // column step of a `refine` pass (rt_render_pass; never a scene feature)
+  FT_ALL = 511
 };
 
 __constant__ int c_perm[256];
@@ -1869,15 +1870,19 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   const int lane = threadIdx.x;
   const int G = P.G;
   const int j = lane & (G - 1), pl = lane / G;
-  const int tilesX = (P.W + P.tw - 1) / P.tw;
+  // columns 0, colStep, ... of a refine pass; the other kernels render every column (the
+  // column-step arithmetic alone cost the C3 kernel 2.4 %)
+  const int ncols = (F & FT_PASS) ? (P.W + P.colStep - 1) / P.colStep : P.W;
+  const int tilesX = (ncols + P.tw - 1) / P.tw;
   int tile = tile_of_block(blockIdx.x, tilesX * ((P.nrows + P.th - 1) / P.th));
   if (tile < 0) return;  // padding block of the XCD mapping (whole workgroup)
   if (P.order) tile = P.order[tile];
   const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();  // wave start (tcost / timeline)
   const int tx = tile % tilesX, ty = tile / tilesX;
-  const int col = tx * P.tw + pl % P.tw;
+  const int ci = tx * P.tw + pl % P.tw;  // column index within this render's columns
+  const int col = (F & FT_PASS) ? ci * P.colStep : ci;
   const int ri = ty * P.th + pl / P.tw;  // row index within this render's rows
-  const bool valid = col < P.W && ri < P.nrows;
+  const bool valid = ci < ncols && ri < P.nrows;
   Counters ct;
   if (CNT)
     for (int i = 0; i < P_N; ++i) ct.c[i] = 0;
@@ -1986,7 +1991,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   }
   if (valid && j == 0) {
     V c = (n == 1 && !dof) ? c1 : clampc(mk(rs / n, gs / n, bs / n));
-    const size_t o = (size_t)ri * P.W + col;
+    const size_t o = (size_t)ri * ncols + ci;
     if (rgb) {
       rgb[3 * o + 0] = (float)c.x;
       rgb[3 * o + 1] = (float)c.y;
@@ -2025,8 +2030,9 @@ template <uint32_t F>
 __global__ void __launch_bounds__(64) probe_kernel(SceneD S, ParamsD P, uint32_t* __restrict__ cost, int ntiles) {
   const int t = blockIdx.x * 64 + threadIdx.x;
   if (t >= ntiles) return;
-  const int tilesX = (P.W + P.tw - 1) / P.tw;
-  const int col = (t % tilesX) * P.tw, ri = (t / tilesX) * P.th;
+  const int ncols = (P.W + P.colStep - 1) / P.colStep;
+  const int tilesX = (ncols + P.tw - 1) / P.tw;
+  const int col = (t % tilesX) * P.tw * P.colStep, ri = (t / tilesX) * P.th;
   const int row = P.row0 + (ri / P.band) * P.rowStep * P.band + ri % P.band;
   Counters ct;
   for (int i = 0; i < P_N; ++i) ct.c[i] = 0;

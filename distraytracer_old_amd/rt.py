@@ -39,7 +39,8 @@ class RenderParams(ctypes.Structure):
 EXPORTS = ["rt_abi_version", "rt_last_error", "rt_device_count", "rt_scene_create", "rt_scene_load_cli",
            "rt_scene_inspect_cli",
            "rt_scene_info", "rt_scene_destroy", "rt_photons_build", "rt_render", "rt_render_device",
-           "rt_render_count", "rt_time_render", "rt_scene_photons", "rt_scene_photon_map", "rt_photons_shoot",
+           "rt_render_count", "rt_time_render", "rt_render_pass", "rt_refine_steps", "rt_scene_photons",
+           "rt_scene_photon_map", "rt_photons_shoot",
            "rt_photons_set",
            "rt_png_name", "rt_scene_save_name"]
 
@@ -77,6 +78,9 @@ def lib():
                                           ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
                                           ctypes.POINTER(ctypes.c_int32)]
         L.rt_photons_shoot.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+        L.rt_refine_steps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        L.rt_render_pass.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_void_p]
         L.rt_photons_set.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         L.rt_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_void_p]
         L.rt_render_count.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p,
@@ -223,6 +227,22 @@ class Scene:
         argb = np.zeros((n, W), dtype=np.int32)
         _check(lib().rt_render(self._h, ctypes.byref(p), rgb.ctypes.data, argb.ctypes.data), "rt_render")
         return rgb, argb
+
+    def refine_steps(self, W, H) -> list[int]:
+        """The `refine on` pass steps of a W x H render (myScene.setRefine); [1] without refine."""
+        buf = np.zeros(16, dtype=np.int32)
+        n = lib().rt_refine_steps(self._h, W, H, buf.ctypes.data, 16)
+        if n < 0:
+            raise RTError(f"rt_refine_steps: {lib().rt_last_error().decode()}")
+        return buf[:n].tolist()
+
+    def render_pass(self, W, H, step, skip_origin, rgb, argb, spp=0, seed=0x5EED0001, flags=0):
+        """One refine pass into full-size host buffers rgb [H, W, 3] float32 / argb [H, W] int32 (in place)."""
+        p = params(W, H, spp, seed, None, 1, flags, 1)
+        assert rgb.shape == (H, W, 3) and rgb.dtype == np.float32 and rgb.flags.c_contiguous
+        assert argb.shape == (H, W) and argb.dtype == np.int32 and argb.flags.c_contiguous
+        _check(lib().rt_render_pass(self._h, ctypes.byref(p), step, int(bool(skip_origin)), rgb.ctypes.data,
+                                    argb.ctypes.data), "rt_render_pass")
 
     def render_count(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, row_band=1):
         p = params(W, H, spp, seed, rows, row_step, 0, row_band)

@@ -239,6 +239,17 @@ int rt_render(rt_scene* scene, const rt_render_params* p, float* rgb, int32_t* a
    and records its waves' durations; the next render of that layout synchronises once and orders the
    tiles by those measured times (longest first). Render a layout twice before timing it. */
 int rt_render_device(rt_scene* scene, const rt_render_params* p, float* d_rgb, int32_t* d_argb, void* hip_stream);
+/* `refine on` (myScene.setRefine, myScene.java:796-803): the progressive steps of a width x height
+   render, largest first and ending at 1 (e.g. 16 8 4 2 1 at 300x300); returns their number n and
+   copies min(n, cap) of them; n = 1 (steps {1}) when the scene does not refine. */
+int rt_refine_steps(const rt_scene* scene, int width, int height, int* steps, int cap);
+/* One refine pass of myFOVScene.draw (myScene.java:1481-1531; the other cameras alike): renders the
+   pixels whose row and column are multiples of `step` and writes each over its step x step span
+   (writePxlSpan, :1171-1177) into full-size HOST buffers rgb[height*width*3] / argb[height*width]
+   (either may be NULL; other pixels are left untouched). skip_origin leaves pixel (0,0) alone (the
+   reference skips it on every pass after the first). p's row fields are ignored. Pixel RNG keys are
+   the full render's, so the passes 16, 8, ..., 1 end in rt_render's image. */
+int rt_render_pass(rt_scene* scene, const rt_render_params* p, int step, int skip_origin, float* rgb, int32_t* argb);
 /* Instrumented render (per-lane counters, RT_ST_*): same image, slower; stats: uint64[RT_ST_N]. */
 int rt_render_count(rt_scene* scene, const rt_render_params* p, float* rgb, int32_t* argb, uint64_t* stats);
 /* Kernel-only timing helper: average ms of the render kernel over `iters` launches (HIP events on the

@@ -277,3 +277,30 @@ def test_top_level_culling_does_not_change_the_image(cli, W, spp):
     a, aa = g.render(W, W, spp=spp, seed=SEED)
     b, ab = g.render(W, W, spp=spp, seed=SEED, flags=rt.RENDER_NOCULL)
     assert np.array_equal(aa, ab) and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("cli,W,spp", [("plnts3ColsBunnies.cli", 96, 2), ("c5Fish.cli", 80, 1),
+                                       ("planets3Ortho.cli", 80, 1), ("t11.cli", 64, 1)])
+def test_refine_passes(cli, W, spp):
+    """`refine on` (myScene.setRefine + draw, myScene.java:796-803,1481-1531): the reference's
+    steps for the image size; after each pass every pixel holds the colour of the pass's sample
+    at the top-left of its step x step span (writePxlSpan; (0,0) skipped after the first pass),
+    and the last pass leaves exactly the plain render's image."""
+    g = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+    assert g.refine_steps(300, 300) == [16, 8, 4, 2, 1]
+    assert g.refine_steps(1024, 1024) == [64, 32, 16, 8, 4, 2, 1]
+    full, fa = g.render(W, W, spp=spp, seed=SEED)
+    rgb = np.zeros((W, W, 3), np.float32)
+    argb = np.zeros((W, W), np.int32)
+    steps = g.refine_steps(W, W)
+    assert steps[-1] == 1 and len(steps) >= 2
+    for k, s in enumerate(steps):
+        g.render_pass(W, W, s, k > 0, rgb, argb, spp=spp, seed=SEED)
+        idx = (np.arange(W) // s) * s
+        assert np.array_equal(argb, fa[np.ix_(idx, idx)]), (cli, s)
+        assert np.array_equal(rgb.view(np.uint32), full[np.ix_(idx, idx)].view(np.uint32)), (cli, s)
+
+
+def test_refine_off_is_one_pass():
+    g = rt.Scene.load_cli("c3_bun69k.cli", textures=scenes.prepare("c3_bun69k.cli"))
+    assert g.refine_steps(1024, 1024) == [1]
