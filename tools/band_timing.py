@@ -8,16 +8,18 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from distraytracer_old_amd import multigpu, rt, scenes  # noqa: E402
 
+BANDS = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [multigpu.BAND]
+ORDERS = ((0, "schedule"), (rt.RENDER_ROWMAJOR, "row-major")) if len(sys.argv) <= 1 else ((0, "schedule"),)
 scenes.ensure_bun69k()
 s = rt.Scene.load_cli("c3_bun69k.cli", textures=scenes.prepare("c3_bun69k.cli"))
-for flags, name in ((0, "schedule"), (rt.RENDER_ROWMAJOR, "row-major")):
+for flags, name in ORDERS:
     full = s.time_render(1024, 1024, spp=16, seed=0x5EED0001, iters=5, flags=flags)
     print(name, "full %.3f ms" % full)
-    for world in (2, 4, 8):
+    for band, world in [(b, w) for b in BANDS for w in (2, 4, 8)]:
         ts = []
         for rank in range(world):
-            r0, r1, step, b = multigpu.rows_of(rank, world, 1024)
+            r0, r1, step, b = multigpu.rows_of(rank, world, 1024, band)
             ts.append(s.time_render(1024, 1024, spp=16, seed=0x5EED0001, rows=(r0, r1), row_step=step, row_band=b,
                                     iters=5, flags=flags))
-        print(" ", world, "max %.3f mean %.3f ideal %.3f eff %.3f" % (max(ts), sum(ts) / len(ts), full / world,
+        print(" ", "band", band, "N", world, "max %.3f mean %.3f ideal %.3f eff %.3f" % (max(ts), sum(ts) / len(ts), full / world,
                                                                        full / world / max(ts)))
