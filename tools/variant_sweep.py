@@ -39,7 +39,7 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "pkstat": ["RT_PROF_PKSTAT"],             # packet lane utilisation (tools/pkstat.py)
 }
 FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS", "g": "RT_MAX_G", "p": "RT_PACKET",
-          "l": "RT_PK_LDS", "b": "RT_PH_BATCH"}
+          "l": "RT_PK_LDS", "b": "RT_PH_BATCH", "m": "RT_PK_MASKED"}
 
 
 def defines_of(name: str) -> list[str]:
