@@ -27,9 +27,13 @@ _lib = None
 
 
 def build(force: bool = False) -> Path:
-    """Compile the oracle with its Makefile (gcc, -ffp-contract=off)."""
-    if force or not LIB_PATH.exists():
-        subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
+    """Compile the oracle with its Makefile (gcc, -ffp-contract=off). make rebuilds only when a
+    source is newer than the library; on the GPU box (no compiler run wanted) a present library
+    is used as shipped."""
+    src_newer = LIB_PATH.exists() and any(
+        f.stat().st_mtime > LIB_PATH.stat().st_mtime for f in (ORACLE_DIR / "src").iterdir())
+    if force or not LIB_PATH.exists() or src_newer:
+        subprocess.run(["make", "-C", str(ORACLE_DIR)] + (["-B"] if force else []), check=True, capture_output=True)
     return LIB_PATH
 
 
@@ -49,6 +53,7 @@ def lib():
         L.oracle_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_int]
+        L.oracle_camera_hits.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -95,6 +100,15 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError("oracle render failed")
         return rgb, argb, dict(zip(ST_NAMES, st[: len(ST_NAMES)].tolist()))
+
+    def camera_hits(self, W: int, H: int, threads: int = 0) -> np.ndarray:
+        """uint8 [H, W]: 1 where the un-jittered FOV camera ray hits an object, 0 where it
+        falls through to the background / skydome (myScene.java:907-914)."""
+        m = np.zeros((H, W), dtype=np.uint8)
+        nt = threads if threads > 0 else min(16, os.cpu_count() or 1)
+        if lib().oracle_camera_hits(self._h, W, H, m.ctypes.data, nt) != 0:
+            raise RuntimeError("oracle_camera_hits: " + lib().oracle_last_error().decode())
+        return m
 
     def close(self):
         if self._h:

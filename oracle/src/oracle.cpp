@@ -2375,4 +2375,27 @@ int oracle_render(void* p, int W, int H, int spp, uint64_t seed, int row0, int r
   return 0;
 }
 
+// Camera-ray hit mask of a W x H FOV render at 1 spp (myFOVScene.draw, myScene.java:1498-1508):
+// mask[row*W+col] = 1 where the un-jittered camera ray hits an object, 0 where it falls through
+// to the background / skydome (reflectRay, :907-914). Used to derive the sky-pixel fixture pinned
+// to the reference's own t11_sierp.png (tests/golden/make_sky_pin.py).
+int oracle_camera_hits(void* p, int W, int H, uint8_t* mask, int nthreads) {
+  Scene* s = (Scene*)p;
+  if (s->camType != 0 || s->hasDOF) { g_err = "oracle_camera_hits: FOV camera without lens only"; return -1; }
+  double fovRad = M_PI * s->fov / 180.0;
+  if (std::fabs(s->fov - 180) < .001) fovRad -= .0001;
+  const double viewZ = -1 * (std::max(H, W) / 2.0) / std::tan(fovRad / 2);
+  const double rayYOffset = H / 2.0, rayXOffset = W / 2.0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int row = 0; row < H; ++row) {
+    uint64_t st[ST_N] = {0};
+    for (int col = 0; col < W; ++col) {
+      Ray r(V3(0, 0, 0), V3(col - rayXOffset, (-1 * (row - rayYOffset)), viewZ), 0);
+      r.key.pixel = (uint64_t)row * (uint64_t)W + (uint64_t)col; r.key.sample = 0; r.key.node = 1;
+      mask[(size_t)row * W + col] = closest_hit(s, r, st).isHit ? 1 : 0;
+    }
+  }
+  return 0;
+}
+
 }  // extern "C"
