@@ -40,6 +40,7 @@ sys.path.insert(0, str(REPO))
 
 METRIC = "Mray/s + achieved HBM GB/s, bun69k.cli 1024² 16spp, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_COPY_PEAK_GBPS = 6300.0  # measured float4-copy peak (MI355X_MICROARCH.md)
 
 # Algorithmic bytes per counted event: SURVEY.md 8(d)'s per-ray formula, records at the
 # sizes it states and no cache credit:
@@ -107,6 +108,28 @@ def cpu_baseline(cli, W, H, spp, seed, tex, row_step=1, threads=16):
     }
 
 
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) started directly: start N ranks as ONE child process tree
+    (torch.distributed.run, one rank per GPU, 127.0.0.1 rendezvous) and return its exit code.
+    Nothing here touches the GPU (device_count does not initialise HIP on this image)."""
+    import socket
+    import subprocess
+
+    import torch
+
+    have = torch.cuda.device_count()
+    if args.backend == "nccl" and have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {have}", file=sys.stderr)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(REPO / "bench.py"), *sys.argv[1:]]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,79 +137,81 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the N-rank step on fewer GPUs (tiles staged to host; ranks share devices)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
 
     import torch
 
-    from distraytracer_old_amd import rt, scenes
+    from distraytracer_old_amd import multigpu, rt, scenes
 
     cli, W, H, spp, seed = scenes.CONFIGS[args.config]
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        print("bench.py: no GPU visible", file=sys.stderr)
+        sys.exit(2)
+    dev = local if args.backend == "nccl" else local % ndev
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
+    coll_dev = "cuda" if args.backend == "nccl" else "cpu"  # where collectives' tensors live
 
     tex = scenes.prepare(cli)
-    scene = rt.Scene.load_cli(cli, textures=tex, device=local)
+    # host-side parse + flatten + BVH build alone (rt_scene_inspect_cli: no device), then the full
+    # scene load (the same host build + upload to HBM); both outside the scaling metric
+    t = time.perf_counter()
+    rt.inspect_cli(cli, textures=tex)
+    host_build_s = time.perf_counter() - t
+    t = time.perf_counter()
+    scene = rt.Scene.load_cli(cli, textures=tex, device=dev)
+    scene_load_s = time.perf_counter() - t
     info = scene.info()
+    photon_s = None
     if info["photon_mode"]:  # photon pre-pass (initRender), outside the timed region; sharded over ranks
-        from distraytracer_old_amd import multigpu as _mg
-        _mg.build_photons_sharded(scene, seed, info["photon_count"], dist)
-    # this rank's rows: r, r+N, ...
-    from distraytracer_old_amd import multigpu
-    r0, r1, step, band = multigpu.rows_of(rank, world, H)
-    p = rt.params(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=step, row_band=band)
-    nrows = rt.nrows_of(p)
-    maxrows = multigpu.max_tile_rows(world, H)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        multigpu.build_photons_sharded(scene, seed, info["photon_count"], dist, device=coll_dev)
+        torch.cuda.synchronize()
+        photon_s = time.perf_counter() - t
+    rr = multigpu.RankRenderer(scene, W, H, spp, seed, dist, stage_host=(args.backend == "gloo"))
+    r0, r1, rstep, band = rr.rows
 
     # exact per-frame counters (instrumented run, outside the timed region)
-    _, _, st = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=step, row_band=band)
-    counts = torch.tensor([traced_rays(st), algorithmic_bytes(st), st["camera"]], dtype=torch.float64, device="cuda")
+    _, _, st = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=rstep, row_band=band)
+    counts = torch.tensor([traced_rays(st), algorithmic_bytes(st), st["camera"]], dtype=torch.float64,
+                          device=coll_dev)
     if dist:
         dist.all_reduce(counts)
     rays_frame, bytes_frame, cam_frame = [float(x) for x in counts.tolist()]
     my_bytes = float(algorithmic_bytes(st))
 
-    rgb = torch.empty((maxrows, W, 3), dtype=torch.float32, device="cuda")
-    argb = torch.empty((maxrows, W), dtype=torch.int32, device="cuda")
-    stream = torch.cuda.current_stream()
-    # N > 1: the single exchange -- float-RGB tiles gathered to rank 0 over RCCL and re-interleaved
-    # there -- pipelined against the next frame's render (multigpu.FrameExchange)
-    ex = multigpu.FrameExchange(dist, H, (maxrows, W, 3), "cuda") if dist else None
-
-    def step(ev=None):
-        def render(tile):
-            if ev:
-                ev[0].record(stream)
-            scene.render_device(p, tile.data_ptr(), argb.data_ptr(), stream.cuda_stream)
-            if ev:
-                ev[1].record(stream)
-        if ex:
-            ex.step(render)
-        else:
-            render(rgb)
-
     # setup (untimed, like the counting run): a layout's first two renders calibrate its tile
     # dispatch order (probe, then measured wave times; rt_render_device in include/distraytracer.h)
-    for _ in range(2):
-        scene.render_device(p, rgb.data_ptr(), argb.data_ptr(), stream.cuda_stream)
-    torch.cuda.synchronize()
+    rr.calibrate()
     # ... then ~0.2 s of untimed frames: the GPU's clocks ramp over the first few launches
     t_warm = time.perf_counter()
     while time.perf_counter() - t_warm < 0.2:
-        scene.render_device(p, rgb.data_ptr(), argb.data_ptr(), stream.cuda_stream)
+        rr.render(rr.rgb)
         torch.cuda.synchronize()
     for _ in range(args.warmup):
-        step()
-    if ex:
-        ex.finish()
+        rr.step()
+    rr.finish()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -194,9 +219,8 @@ def main():
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(evs[i])
-    if ex:
-        ex.finish()  # the last frame's gather + assemble are inside the timed region
+        rr.step(evs[i])
+    rr.finish()  # the last frame's gather + assemble are inside the timed region
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -204,7 +228,7 @@ def main():
     dt = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
 
-    t = torch.tensor([dt, kern_ms], dtype=torch.float64, device="cuda")
+    t = torch.tensor([dt, kern_ms], dtype=torch.float64, device=coll_dev)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, kern_ms_max = t.tolist()
@@ -214,7 +238,7 @@ def main():
         # rank-0 kernel: its own algorithmic bytes over its own mean kernel duration
         achieved = my_bytes / (kern_ms / 1e3) / 1e9
         workload = f"{args.config} {cli} {W}x{H} {spp}spp"
-        traffic, tsrc = find_traffic(workload)
+        traffic, tsrc = find_traffic(workload) if world == 1 else (None, None)
         out = {
             "metric": METRIC,
             "value": rays_frame / (ms_per_step / 1e3) / 1e6,
@@ -233,17 +257,27 @@ def main():
             "config": {"workload": workload, "width": W, "height": H, "spp": spp, "seed": seed,
                        "rays_per_frame": int(rays_frame), "camera_samples": int(cam_frame),
                        "parallelism": f"{multigpu.BAND}-row bands interleaved over {world} rank(s)" +
-                                      (" + RCCL gather of float RGB tiles to rank 0" if world > 1 else "")},
+                                      (f" + {args.backend} gather of float RGB tiles to rank 0" if world > 1 else "")},
             "camera_msamples_per_s": cam_frame / (ms_per_step / 1e3) / 1e6,
+            "kernel_ms_max_over_ranks": kern_ms_max,
+            "host_build_s": host_build_s,
+            "scene_load_s": scene_load_s,
+            "photon_prepass_s": photon_s,
             "achieved_hbm_gbps": achieved,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
+                         "frac_vs_measured_copy_peak": achieved / HBM_COPY_PEAK_GBPS,
                          "traffic": traffic, "traffic_source": tsrc,
                          "kernel": "render_kernel", "kernel_ms": kern_ms,
                          "bytes_per_launch": my_bytes, "bytes_per_ray": bytes_frame / max(1.0, rays_frame)},
         }
+        if world > 1 and args.backend == "gloo":
+            out["rehearsal"] = f"gloo backend, {world} ranks on {ndev} GPU(s): not a scaling measurement"
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cli, W, H, spp, seed, tex)
+            cb = cpu_baseline(cli, W, H, spp, seed, tex)
+            cb["frame_s_1thread_extrapolated"] = rays_frame / (cb["value_1thread"] * 1e6)
+            out["cpu_baseline"] = cb
+        assert out["n_gpus"] == args.gpus
         print(json.dumps(out), flush=True)
     scene.close()
     if dist:

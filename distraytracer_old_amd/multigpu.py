@@ -142,9 +142,31 @@ def merge_photon_shards(shards):
     return np.concatenate(pos), np.concatenate(pwr)
 
 
-def build_photons_sharded(scene, seed: int, count: int, dist=None):
-    """The photon pre-pass split over ranks: each rank shoots its index range,
-    the shards are all-gathered, every rank builds the same photon map."""
+def _all_gather_rows(dist, rows, device):
+    """All-gather a ragged float64 array [n_r, C] from every rank -> list of [n_r, C] numpy arrays
+    in rank order: counts first, then one all_gather of the tiles padded to the largest count
+    (on `device`: the GPU under RCCL, the host under gloo)."""
+    import numpy as np
+    import torch
+
+    world = dist.get_world_size()
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    ns = [int(x.item()) for x in ns]
+    cap = max(1, max(ns))
+    buf = torch.zeros((cap, rows.shape[1]), dtype=torch.float64, device=device)
+    buf[: rows.shape[0]] = torch.from_numpy(np.ascontiguousarray(rows)).to(device)
+    outs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(outs, buf)
+    return [o[:k].cpu().numpy() for o, k in zip(outs, ns)]
+
+
+def build_photons_sharded(scene, seed: int, count: int, dist=None, device="cuda"):
+    """The photon pre-pass split over ranks: each rank shoots its emitted-photon
+    index range, the shards (positions, powers, per-light counts) are all-gathered as tensors
+    (RCCL on `device`), merged into the reference's photon_list order, and every rank builds
+    the same photon map."""
     import numpy as np
 
     rank = dist.get_rank() if dist else 0
@@ -154,9 +176,78 @@ def build_photons_sharded(scene, seed: int, count: int, dist=None):
     if dist is None:
         shards = [(pos, pwr, per)]
     else:
-        objs = [None] * world
-        dist.all_gather_object(objs, (pos, pwr, per))
-        shards = objs
+        rec = _all_gather_rows(dist, np.concatenate([pos.reshape(-1, 3), pwr.reshape(-1, 3)], 1), device)
+        pers = _all_gather_rows(dist, np.asarray(per, dtype=np.float64).reshape(1, -1), device)
+        shards = [(r[:, :3], r[:, 3:], pl[0].astype(np.int64)) for r, pl in zip(rec, pers)]
     full_pos, full_pwr = merge_photon_shards(shards)
     scene.set_photons(full_pos, full_pwr)
     return len(full_pos)
+
+
+class RankRenderer:
+    """One rank's share of bench.py's N-GPU step: renders the rank's row bands (rows_of) with
+    the HIP kernel into a device tile on the current stream (rt_render_device), and with N > 1
+    hands the tile to FrameExchange (gathered to rank 0 and re-interleaved there, pipelined
+    against the next frame). `stage_host`: copy the tile to host memory before the exchange
+    (the gloo backend, which cannot gather device tensors; used to run this exact path as
+    several processes on one GPU).
+
+      rr = RankRenderer(scene, W, H, spp, seed, dist)
+      rr.calibrate()                 # untimed: the layout's tile-schedule calibration renders
+      for each frame: rr.step()      # optional (start, end) HIP events around the kernel
+      img = rr.finish()              # rank 0: the last assembled frame [H, W, 3] (device / host)
+    """
+
+    def __init__(self, scene, W, H, spp, seed, dist=None, stage_host=False, band=BAND):
+        import torch
+
+        from . import rt
+
+        self.scene, self.W, self.H = scene, W, H
+        self.dist = dist
+        self.rank = dist.get_rank() if dist else 0
+        self.world = dist.get_world_size() if dist else 1
+        r0, r1, step, b = rows_of(self.rank, self.world, H, band)
+        self.p = rt.params(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=step, row_band=b)
+        self.rows = (r0, r1, step, b)
+        self.maxrows = max_tile_rows(self.world, H, band)
+        assert rt.nrows_of(self.p) <= self.maxrows
+        self.rgb = torch.empty((self.maxrows, W, 3), dtype=torch.float32, device="cuda")
+        self.argb = torch.empty((self.maxrows, W), dtype=torch.int32, device="cuda")
+        self.stream = torch.cuda.current_stream()
+        self.stage_host = stage_host
+        self.ex = None
+        if dist is not None and self.world > 1:
+            self.ex = FrameExchange(dist, H, (self.maxrows, W, 3), "cpu" if stage_host else "cuda", band=band)
+
+    def render(self, tile, ev=None):
+        if ev:
+            ev[0].record(self.stream)
+        self.scene.render_device(self.p, tile.data_ptr(), self.argb.data_ptr(), self.stream.cuda_stream)
+        if ev:
+            ev[1].record(self.stream)
+
+    def calibrate(self, n=2):
+        """A row layout's first two renders order its tiles (probe, then measured wave times)."""
+        import torch
+
+        for _ in range(n):
+            self.render(self.rgb)
+        torch.cuda.synchronize()
+
+    def step(self, ev=None):
+        if self.ex is None:
+            self.render(self.rgb, ev)
+        elif self.stage_host:
+            def render(tile):
+                self.render(self.rgb, ev)
+                tile.copy_(self.rgb)  # device -> host (synchronous), then the gloo gather
+            self.ex.step(render)
+        else:
+            self.ex.step(lambda tile: self.render(tile, ev))
+
+    def finish(self):
+        """Drain the pipelined exchange; rank 0 gets the assembled image [H, W, 3], others None."""
+        if self.ex is not None:
+            return self.ex.finish()
+        return self.rgb[: self.H] if self.rank == 0 else None
