@@ -586,9 +586,9 @@ int rt_render_pass(rt_scene* s, const rt_render_params* p, int step, int skip_or
 }
 
 #ifdef RT_PROF_PKSTAT
-int rt_prof_pkstat_get(uint64_t* out) {  // profiling builds only: read and clear rt_pk_stat[8]
-  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(dv::rt_pk_stat), 8 * sizeof(uint64_t)));
-  const uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+int rt_prof_pkstat_get(uint64_t* out) {  // profiling builds only: read and clear rt_pk_stat[12]
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(dv::rt_pk_stat), 12 * sizeof(uint64_t)));
+  const uint64_t z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dv::rt_pk_stat), z, sizeof(z)));
   return RT_OK;
 }

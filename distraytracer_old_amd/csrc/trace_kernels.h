@@ -128,7 +128,7 @@ DEVI uint64_t uni64(uint64_t v) {
 }
 DEVI bool in_mask(uint64_t m) { return (m >> __lane_id()) & 1; }
 #ifdef RT_PROF_PKSTAT
-__device__ unsigned long long rt_pk_stat[8];
+__device__ unsigned long long rt_pk_stat[12];
 // one wave step testing the lanes in m: counted once per wave (by its first active lane)
 #define PKSTAT(step, m)                                                                   \
   do {                                                                                    \
@@ -1550,6 +1550,7 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     if (CNT) ct.c[C_SHADOW]++;
     Key sk = k;
     sk.tsite = SITE_SHADOW_TIME + li;
+    PKSTAT(P_SH_STEP, __ballot(1));
 #ifdef RT_PROF_NOSHADOW  // profiling builds only (tools/variant_sweep.py): results differ
     if (false)
 #endif
@@ -1778,6 +1779,7 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
 #ifdef RT_PROF_NOTRACE  // profiling builds only (tools/variant_sweep.py): results differ
       Best b = miss();
 #else
+      PKSTAT(P_RAY_STEP, __ballot(1));
       Best b = closest<CNT, F, PACKET>(S, w, k, ct);
 #endif
       if (b.t == DMAX) {

@@ -22,3 +22,11 @@ def compare(rgb_a, argb_a, rgb_b, argb_b, tol=TOL):
         "argb_mismatch_on_good": argb_mis,
         "argb_equal": int((argb_a == argb_b).sum()),
     }
+
+
+def assert_exact_decisions(c):
+    """Every pixel within the per-channel tolerance (no decision mismatch: hit object, shadow,
+    TIR, photon k-set all agree) and every such pixel's ARGB int equal -- what was observed on
+    every deterministic-decision config."""
+    assert c["mismatch"] == 0, c
+    assert c["argb_mismatch_on_good"] == 0, c

@@ -6,7 +6,7 @@ import pytest
 
 from distraytracer_old_amd import scenes
 from tests.golden.make_golden import FIXTURES, render
-from tests.parity import TOL, compare
+from tests.parity import TOL, assert_exact_decisions, compare
 
 import pathlib
 
@@ -36,5 +36,4 @@ def test_gpu_matches_golden(name):
     rgb, argb = s.render(W, H, spp=spp, seed=seed, rows=(r0, r1))
     g_rgb, g_argb = load(name)
     c = compare(rgb[:, c0:c1], argb[:, c0:c1], g_rgb, g_argb, tol=TOL)
-    assert c["mismatch_frac"] < 2e-3, c
-    assert c["argb_mismatch_on_good"] <= max(1, c["pixels"] // 1000), c
+    assert_exact_decisions(c)

@@ -10,7 +10,7 @@ import pytest
 
 from distraytracer_old_amd import rt, scenes
 from oracle.oracle import OracleScene
-from tests.parity import compare
+from tests.parity import assert_exact_decisions, compare
 
 pytestmark = pytest.mark.gpu
 
@@ -47,15 +47,12 @@ def test_c2_shiny_ball_kat_and_parity():
 
 def test_c3_bun69k_small_parity():
     g, o, (rg, ag), (ro, ao) = both("c3_bun69k.cli", 256, 256, 4)
-    c = compare(rg, ag, ro, ao)
-    assert c["mismatch_frac"] < 1e-3, c
-    assert c["argb_mismatch_on_good"] == 0, c
+    assert_exact_decisions(compare(rg, ag, ro, ao))
 
 
 def test_c4_planets_small_parity():
     g, o, (rg, ag), (ro, ao) = both("plnts3ColsBunnies.cli", 160, 160, 2, seed=0x5EED0004)
-    c = compare(rg, ag, ro, ao)
-    assert c["mismatch_frac"] < 2e-3, c
+    assert_exact_decisions(compare(rg, ag, ro, ao))
 
 
 @pytest.mark.parametrize("cli,spp", [("old_t07.cli", 1), ("old_t07.cli", 4), ("old_t10.cli", 1), ("old_t10.cli", 4),
@@ -64,8 +61,7 @@ def test_camera_scenes_parity(cli, spp):
     """orthographic (old_t07, planets3Ortho: textures + glass) and fisheye 180 (old_t10) cameras
     (myOrthoScene / myFishEyeScene, myScene.java:1535-1755), 1 spp and jittered."""
     g, o, (rg, ag), (ro, ao) = both(cli, 96, 96, spp)
-    c = compare(rg, ag, ro, ao)
-    assert c["mismatch_frac"] < 2e-3, c
+    assert_exact_decisions(compare(rg, ag, ro, ao))
     if cli == "old_t10.cli" and spp == 1:  # outside the image circle: blkColor
         assert (int(ag[0, 0]) & 0xFFFFFFFF) == 0xFF000000 and rg[0, 0].max() == 0
 
@@ -77,8 +73,7 @@ def test_feature_scenes_parity(cli, spp):
     procedural wood (p3_t09 = C3 with its wood line; myBaseWoodTexture), wood2 with named
     noise_color (p4_t05; myWoodTexture) and marble with custom noise_color (p4_t06_2)."""
     g, o, (rg, ag), (ro, ao) = both(cli, 128, 128, spp)
-    c = compare(rg, ag, ro, ao)
-    assert c["mismatch_frac"] < 2e-3, c
+    assert_exact_decisions(compare(rg, ag, ro, ao))
 
 
 @pytest.mark.parametrize("cli", [f"p4_st0{i}.cli" for i in range(1, 10)])
@@ -87,8 +82,7 @@ def test_stone_parity(cli):
     the ROI functions 2..8 with Euclid distance, st08 nearestROI with Manhattan distance,
     st09 altExpROI; all read worleyClrs.cli (10 noise colours)."""
     g, o, (rg, ag), (ro, ao) = both(cli, 96, 96, 1)
-    c = compare(rg, ag, ro, ao)
-    assert c["mismatch_frac"] < 2e-3, c
+    assert_exact_decisions(compare(rg, ag, ro, ao))
 
 
 @pytest.mark.parametrize("cli,spp", [("p3_t01.cli", 1), ("p3_t02.cli", 2), ("p3_t03.cli", 1), ("p4_t02.cli", 1),
@@ -101,8 +95,7 @@ def test_instance_parity(cli, spp):
     instances (p3_t02_sierp: 341 spheres; p3_t11_sierp: 21,845 bun69k instances, two-level)."""
     scenes.ensure_bun69k()
     g, o, (rg, ag), (ro, ao) = both(cli, 96, 96, spp)
-    c = compare(rg, ag, ro, ao)
-    assert c["mismatch_frac"] < 2e-3, c
+    assert_exact_decisions(compare(rg, ag, ro, ao))
 
 
 def test_c3_full_size_properties():
@@ -120,8 +113,7 @@ def test_c3_full_size_properties():
     assert np.array_equal(ail, ag[3::8])
     o = OracleScene(scenes.SCENE_DIR, "c3_bun69k.cli", tex)
     ro, ao, _ = o.render(1024, 1024, spp=16, seed=SEED, rows=(5, 1024), row_step=64)
-    c = compare(rg[5::64], ag[5::64], ro, ao)
-    assert c["mismatch_frac"] < 1e-3, c
+    assert_exact_decisions(compare(rg[5::64], ag[5::64], ro, ao))
     assert rg.min() >= 0 and rg.max() <= 1.0
 
 
@@ -131,8 +123,8 @@ def test_ray_counts_match_oracle():
     _, _, sg = g.render_count(128, 128, spp=2, seed=SEED)
     o = OracleScene(scenes.SCENE_DIR, "c3_bun69k.cli", tex)
     _, _, so = o.render(128, 128, spp=2, seed=SEED)
-    for k in ("camera", "shadow", "refl", "refr", "tri", "light"):
-        assert abs(sg[k] - so[k]) <= 1e-3 * max(1, so[k]), (k, sg[k], so[k])
+    for k in ("camera", "shadow", "refl", "refr", "tri", "light", "texel"):
+        assert sg[k] == so[k], (k, sg[k], so[k])
 
 
 @pytest.mark.parametrize("mode,spec", [("diffuse", "diffuse_photons  20000  50 0.1"),
