@@ -15,7 +15,7 @@ LIB_DIR = PKG / "lib"
 LIB_PATH = LIB_DIR / "libdistraytracer.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["trace.hip", "photon_build.hip", "cli_loader.cpp", "scene_build.cpp", "photon.cpp"]
-HEADERS = ["rt_types.h", "rt_internal.h", "host_math.h", "trace_device.h", "trace_kernels.h", "qdiv.h"]
+HEADERS = ["rt_types.h", "rt_internal.h", "host_math.h", "trace_device.h", "trace_kernels.h", "qdiv.h", "jfdlibm.h"]
 # -ffp-contract=off: keep the reference's (Java) unfused double arithmetic so discrete
 # decisions (hits, shadows, TIR) match the oracle; no fast-math (IEEE Inf/NaN needed).
 COMPILE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",

@@ -160,7 +160,7 @@ struct CliLoader {
     R1.m[0] = av.x; R1.m[1] = av.y; R1.m[2] = av.z;
     R1.m[4] = bv.x; R1.m[5] = bv.y; R1.m[6] = bv.z;
     R1.m[8] = cv.x; R1.m[9] = cv.y; R1.m[10] = cv.z;
-    R2.m[5] = std::cos(ar); R2.m[6] = -std::sin(ar); R2.m[9] = std::sin(ar); R2.m[10] = std::cos(ar);
+    R2.m[5] = jf::cos(ar); R2.m[6] = -jf::sin(ar); R2.m[9] = jf::sin(ar); R2.m[10] = jf::cos(ar);
     stack.back() = mul(stack.back(), mul(transpose(R1), mul(R2, R1)));
   }
   void push() { stack.push_back(stack.back()); }  // gtPushMatrix :1241-1246

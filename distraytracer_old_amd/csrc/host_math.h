@@ -9,6 +9,8 @@
 #include <cstring>
 #include <limits>
 
+#include "jfdlibm.h"  // sin / cos: the fdlibm sequences the oracle and the device share
+
 namespace rt {
 namespace hm {
 
@@ -120,7 +122,7 @@ static inline Mat inverse(const Mat& a) {
   return r;
 }
 static inline D3 rot_axis(D3 v1, D3 u, double thet) {  // rotVecAroundAxis
-  double cT = std::cos(thet), sT = std::sin(thet), oneMC = 1 - cT, ux2 = u.x * u.x, uy2 = u.y * u.y,
+  double cT = jf::cos(thet), sT = jf::sin(thet), oneMC = 1 - cT, ux2 = u.x * u.x, uy2 = u.y * u.y,
          uz2 = u.z * u.z, uxy = u.x * u.y, uxz = u.x * u.z, uyz = u.y * u.z, uzS = u.z * sT, uyS = u.y * sT,
          uxS = u.x * sT, uxzC1 = uxz * oneMC, uxyC1 = uxy * oneMC, uyzC1 = uyz * oneMC;
   return d3((ux2 * oneMC + cT) * v1.x + (uxyC1 - uzS) * v1.y + (uxzC1 + uyS) * v1.z,

@@ -1,0 +1,211 @@
+// sin, cos, asin, acos with fdlibm's algorithms (the ones java.lang.StrictMath specifies),
+// written once for BOTH sides of the parity check: the HIP kernels (device) and the
+// oracle's CPU restatement (host, g++) evaluate these exact operation sequences, so every
+// result is bit-identical across device and host -- unlike ocml vs glibc, whose last-bit
+// differences flipped discrete decisions downstream (photon emission / bounce directions,
+// Fresnel TIR, spot-light cut-off; VERDICT r01 Weak #2).
+//
+// Restated from the published fdlibm 5.3 algorithms (k_sin.c, k_cos.c, e_rem_pio2.c,
+// s_sin.c, s_cos.c, e_asin.c, e_acos.c). Differences, all deterministic:
+//  * argument reduction handles |x| <= 2^19 * pi/2 (Cody-Waite, three-part pi/2 with the
+//    cancellation checks of e_rem_pio2.c, without its npio2_hw shortcut table); larger
+//    arguments -- never reached on the trace path, whose angles are draws in [0, 2pi),
+//    acos / asin results or texture coordinates -- are reduced by the same three-part
+//    step with n computed the same way (less accurate there, still identical on both sides);
+//  * no floating-point exception / inexact-flag side effects.
+// tests/test_jfdlibm.py checks these against glibc (correctly rounded in practice) to
+// <= 1 ulp over 2M arguments spanning every branch.
+//
+// Must be compiled without FMA contraction (-ffp-contract=off) on both sides, as the rest
+// of the trace path is.
+#pragma once
+#include <stdint.h>
+
+#ifndef JF_FN
+#if defined(__HIP__)  // HIP language (trace.hip); plain C++ (loader, oracle) otherwise
+#define JF_FN __host__ __device__ inline
+#else
+#define JF_FN static inline
+#endif
+#endif
+
+namespace jf {
+
+JF_FN uint64_t bits(double x) { return __builtin_bit_cast(uint64_t, x); }
+JF_FN double from_bits(uint64_t b) { return __builtin_bit_cast(double, b); }
+JF_FN int32_t hiw(double x) { return (int32_t)(bits(x) >> 32); }
+JF_FN double zero_low(double x) { return from_bits(bits(x) & 0xFFFFFFFF00000000ULL); }
+JF_FN double fabs_(double x) { return from_bits(bits(x) & 0x7FFFFFFFFFFFFFFFULL); }
+JF_FN double sqrt_(double x) { return __builtin_sqrt(x); }  // IEEE correctly rounded on both sides
+
+// k_sin.c: sin(x + y) on [-pi/4, pi/4], y the tail of x; iy = 0 means y is 0
+JF_FN double k_sin(double x, double y, int iy) {
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  const int32_t ix = hiw(x) & 0x7fffffff;
+  if (ix < 0x3e400000) return x;  // |x| < 2^-27
+  const double z = x * x, v = z * x;
+  const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  if (iy == 0) return x + v * (S1 + z * r);
+  return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+
+// k_cos.c: cos(x + y) on [-pi/4, pi/4]
+JF_FN double k_cos(double x, double y) {
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  const int32_t ix = hiw(x) & 0x7fffffff;
+  if (ix < 0x3e400000) return 1.0;  // |x| < 2^-27
+  const double z = x * x;
+  const double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+  if (ix < 0x3FD33333) return 1.0 - (0.5 * z - (z * r - x * y));  // |x| < 0.3
+  const double qx = (ix > 0x3fe90000) ? 0.28125 : from_bits((uint64_t)(uint32_t)(ix - 0x00200000) << 32);  // x/4
+  const double hz = 0.5 * z - qx, a = 1.0 - qx;
+  return a - (hz - (z * r - x * y));
+}
+
+// e_rem_pio2.c (medium range): x - n*pi/2 = y0 + y1, returns n
+JF_FN int rem_pio2(double x, double& y0, double& y1) {
+  const double invpio2 = 6.36619772367581382433e-01;
+  const double pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11;
+  const double pio2_2 = 6.07710050630396597660e-11, pio2_2t = 2.02226624879595063154e-21;
+  const double pio2_3 = 2.02226624871116645580e-21, pio2_3t = 8.47842766036889956997e-32;
+  const int32_t hx = hiw(x), ix = hx & 0x7fffffff;
+  if (ix <= 0x3fe921fb) { y0 = x; y1 = 0; return 0; }  // |x| <= pi/4
+  if (ix < 0x4002d97c) {  // |x| < 3pi/4: n = +-1
+    if (hx > 0) {
+      double z = x - pio2_1;
+      if (ix != 0x3ff921fb) { y0 = z - pio2_1t; y1 = (z - y0) - pio2_1t; }
+      else { z -= pio2_2; y0 = z - pio2_2t; y1 = (z - y0) - pio2_2t; }
+      return 1;
+    }
+    double z = x + pio2_1;
+    if (ix != 0x3ff921fb) { y0 = z + pio2_1t; y1 = (z - y0) + pio2_1t; }
+    else { z += pio2_2; y0 = z + pio2_2t; y1 = (z - y0) + pio2_2t; }
+    return -1;
+  }
+  const double t0 = fabs_(x);
+  const int32_t n = (int32_t)(t0 * invpio2 + 0.5);
+  const double fn = (double)n;
+  double r = t0 - fn * pio2_1, w = fn * pio2_1t;
+  const int32_t j = ix >> 20;
+  y0 = r - w;
+  int32_t i = j - ((hiw(y0) >> 20) & 0x7ff);
+  if (i > 16) {  // 2nd iteration: 118 bits of pi/2
+    double t = r;
+    w = fn * pio2_2;
+    r = t - w;
+    w = fn * pio2_2t - ((t - r) - w);
+    y0 = r - w;
+    i = j - ((hiw(y0) >> 20) & 0x7ff);
+    if (i > 49) {  // 3rd iteration: 151 bits
+      t = r;
+      w = fn * pio2_3;
+      r = t - w;
+      w = fn * pio2_3t - ((t - r) - w);
+      y0 = r - w;
+    }
+  }
+  y1 = (r - y0) - w;
+  if (hx < 0) { y0 = -y0; y1 = -y1; return -n; }
+  return n;
+}
+
+JF_FN double sin(double x) {  // s_sin.c
+  const int32_t ix = hiw(x) & 0x7fffffff;
+  if (ix <= 0x3fe921fb) return k_sin(x, 0.0, 0);
+  if (ix >= 0x7ff00000) return x - x;  // Inf / NaN -> NaN
+  double y0, y1;
+  const int n = rem_pio2(x, y0, y1);
+  switch (n & 3) {
+    case 0: return k_sin(y0, y1, 1);
+    case 1: return k_cos(y0, y1);
+    case 2: return -k_sin(y0, y1, 1);
+    default: return -k_cos(y0, y1);
+  }
+}
+
+JF_FN double cos(double x) {  // s_cos.c
+  const int32_t ix = hiw(x) & 0x7fffffff;
+  if (ix <= 0x3fe921fb) return k_cos(x, 0.0);
+  if (ix >= 0x7ff00000) return x - x;
+  double y0, y1;
+  const int n = rem_pio2(x, y0, y1);
+  switch (n & 3) {
+    case 0: return k_cos(y0, y1);
+    case 1: return -k_sin(y0, y1, 1);
+    case 2: return -k_cos(y0, y1);
+    default: return k_sin(y0, y1, 1);
+  }
+}
+
+// rational approximation shared by e_asin.c / e_acos.c: R(z) = p(z) / q(z)
+JF_FN double asin_p(double z) {
+  const double pS0 = 1.66666666666666657415e-01, pS1 = -3.25565818622400915405e-01,
+               pS2 = 2.01212532134862925881e-01, pS3 = -4.00555345006794114027e-02,
+               pS4 = 7.91534994289814532176e-04, pS5 = 3.47933107596021167570e-05;
+  return z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+}
+JF_FN double asin_q(double z) {
+  const double qS1 = -2.40339491173441421878e+00, qS2 = 2.02094576023350569471e+00,
+               qS3 = -6.88283971605453293030e-01, qS4 = 7.70381505559019352791e-02;
+  return 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+}
+
+JF_FN double acos(double x) {  // e_acos.c
+  const double pi = 3.14159265358979311600e+00, pio2_hi = 1.57079632679489655800e+00,
+               pio2_lo = 6.12323399573676603587e-17;
+  const int32_t hx = hiw(x), ix = hx & 0x7fffffff;
+  if (ix >= 0x3ff00000) {  // |x| >= 1
+    if (((ix - 0x3ff00000) | (int32_t)(uint32_t)bits(x)) == 0) return hx > 0 ? 0.0 : pi + 2.0 * pio2_lo;
+    return (x - x) / (x - x);  // NaN
+  }
+  if (ix < 0x3fe00000) {  // |x| < 0.5
+    if (ix <= 0x3c600000) return pio2_hi + pio2_lo;  // |x| < 2^-57
+    const double z = x * x, r = asin_p(z) / asin_q(z);
+    return pio2_hi - (x - (pio2_lo - x * r));
+  }
+  if (hx < 0) {  // x < -0.5
+    const double z = (1.0 + x) * 0.5, s = sqrt_(z), r = asin_p(z) / asin_q(z);
+    const double w = r * s - pio2_lo;
+    return pi - 2.0 * (s + w);
+  }
+  const double z = (1.0 - x) * 0.5, s = sqrt_(z), df = zero_low(s);  // x > 0.5
+  const double c = (z - df * df) / (s + df);
+  const double r = asin_p(z) / asin_q(z), w = r * s + c;
+  return 2.0 * (df + w);
+}
+
+JF_FN double asin(double x) {  // e_asin.c
+  const double pio2_hi = 1.57079632679489655800e+00, pio2_lo = 6.12323399573676603587e-17,
+               pio4_hi = 7.85398163397448278999e-01;
+  const int32_t hx = hiw(x), ix = hx & 0x7fffffff;
+  if (ix >= 0x3ff00000) {  // |x| >= 1
+    if (((ix - 0x3ff00000) | (int32_t)(uint32_t)bits(x)) == 0) return x * pio2_hi + x * pio2_lo;
+    return (x - x) / (x - x);
+  }
+  if (ix < 0x3fe00000) {  // |x| < 0.5
+    if (ix < 0x3e400000) return x;  // |x| < 2^-27
+    const double t = x * x, w = asin_p(t) / asin_q(t);
+    return x + x * w;
+  }
+  const double w0 = 1.0 - fabs_(x), t = w0 * 0.5;  // 0.5 <= |x| < 1
+  const double p = asin_p(t), q = asin_q(t), s = sqrt_(t);
+  double res;
+  if (ix >= 0x3FEF3333) {  // |x| > 0.975
+    const double w = p / q;
+    res = pio2_hi - (2.0 * (s + s * w) - pio2_lo);
+  } else {
+    const double w = zero_low(s);
+    const double c = (t - w * w) / (s + w);
+    const double r = p / q;
+    const double pp = 2.0 * s * r - (pio2_lo - 2.0 * c);
+    const double qq = pio4_hi - 2.0 * w;
+    res = pio4_hi - (pp - qq);
+  }
+  return hx > 0 ? res : -res;
+}
+
+}  // namespace jf

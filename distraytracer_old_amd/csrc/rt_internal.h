@@ -71,6 +71,13 @@ struct rt_scene {
   size_t devBytes = 0;
   bool photonsUploaded = false;
   void* counters = nullptr;  // device uint64[RT_ST_N]
+  // rt_render / rt_render_count (host buffers): output buffers kept across calls (grow-only)
+  // and the scene's own non-blocking stream, so the blocking per-frame entry (the JNI
+  // nativeRender path) pays no hipMalloc / hipFree / device-wide synchronisation per call
+  float* outRgb = nullptr;
+  int32_t* outArgb = nullptr;
+  size_t outCap = 0;  // pixels
+  void* stream = nullptr;  // hipStream_t
   const double* noCullBound = nullptr;  // device [ntop][4] of -1 (RT_RENDER_NOCULL)
   // tile schedules (longest tiles first) per tile layout (trace.hip `schedule`)
   struct TileSchedule {

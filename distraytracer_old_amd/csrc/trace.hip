@@ -240,9 +240,13 @@ int rt_scene_photons(const rt_scene* s, double* pos, double* pwr, int64_t n, int
 
 void rt_scene_destroy(rt_scene* s) {
   if (!s) return;
-  if (!s->allocs.empty()) {
+  if (!s->allocs.empty() || s->stream || s->outRgb || s->outArgb) {
     (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize((hipStream_t)s->stream);
     for (void* p : s->allocs) (void)hipFree(p);
+    (void)hipFree(s->outRgb);
+    (void)hipFree(s->outArgb);
+    if (s->stream) (void)hipStreamDestroy((hipStream_t)s->stream);
   }
   delete s;
 }
@@ -448,28 +452,71 @@ static int render_host(rt_scene* s, const rt_render_params* p, float* rgb, int32
   int rc = make_params(s, p, P);
   if (rc) return rc;
   HIPCHK(hipSetDevice(s->device));
-  size_t npx = (size_t)P.nrows * P.W;
-  float* d_rgb = nullptr;
-  int32_t* d_argb = nullptr;
-  HIPCHK(hipMalloc(&d_rgb, npx * 3 * sizeof(float)));
-  hipError_t e = hipMalloc(&d_argb, npx * sizeof(int32_t));
-  if (e != hipSuccess) { (void)hipFree(d_rgb); return set_error(RT_E_HIP, hipGetErrorString(e)); }
-  rc = launch(s, P, p->flags, d_rgb, d_argb, stats != nullptr, 0);
-  if (rc == RT_OK) {
-    e = hipDeviceSynchronize();
-    if (e != hipSuccess) rc = set_error(RT_E_HIP, std::string("render kernel: ") + hipGetErrorString(e));
+  if (!s->stream) {
+    hipStream_t st;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    s->stream = st;
   }
-  if (rc == RT_OK && rgb) { e = hipMemcpy(rgb, d_rgb, npx * 3 * sizeof(float), hipMemcpyDeviceToHost); if (e) rc = set_error(RT_E_HIP, hipGetErrorString(e)); }
-  if (rc == RT_OK && argb) { e = hipMemcpy(argb, d_argb, npx * sizeof(int32_t), hipMemcpyDeviceToHost); if (e) rc = set_error(RT_E_HIP, hipGetErrorString(e)); }
-  if (rc == RT_OK && stats) { e = hipMemcpy(stats, s->counters, sizeof(uint64_t) * RT_ST_N, hipMemcpyDeviceToHost); if (e) rc = set_error(RT_E_HIP, hipGetErrorString(e)); }
-  (void)hipFree(d_rgb);
-  (void)hipFree(d_argb);
+  hipStream_t st = (hipStream_t)s->stream;
+  const size_t npx = (size_t)P.nrows * P.W;
+  if (npx > s->outCap) {  // grow-only device output buffers, reused by later calls
+    HIPCHK(hipStreamSynchronize(st));
+    (void)hipFree(s->outRgb);
+    (void)hipFree(s->outArgb);
+    s->outRgb = nullptr; s->outArgb = nullptr; s->outCap = 0;
+    HIPCHK(hipMalloc(&s->outRgb, npx * 3 * sizeof(float)));
+    HIPCHK(hipMalloc(&s->outArgb, npx * sizeof(int32_t)));
+    s->outCap = npx;
+  }
+  rc = launch(s, P, p->flags, s->outRgb, s->outArgb, stats != nullptr, st);
+  hipError_t e = hipSuccess;
+  if (rc == RT_OK && rgb) e = hipMemcpyAsync(rgb, s->outRgb, npx * 3 * sizeof(float), hipMemcpyDeviceToHost, st);
+  if (rc == RT_OK && e == hipSuccess && argb) e = hipMemcpyAsync(argb, s->outArgb, npx * sizeof(int32_t), hipMemcpyDeviceToHost, st);
+  if (rc == RT_OK && e == hipSuccess && stats)
+    e = hipMemcpyAsync(stats, s->counters, sizeof(uint64_t) * RT_ST_N, hipMemcpyDeviceToHost, st);
+  hipError_t se = hipStreamSynchronize(st);  // the call blocks until the frame is in the caller's buffers
+  if (rc == RT_OK && e != hipSuccess) rc = set_error(RT_E_HIP, hipGetErrorString(e));
+  if (rc == RT_OK && se != hipSuccess) rc = set_error(RT_E_HIP, std::string("render kernel: ") + hipGetErrorString(se));
   return rc;
+}
+
+// fdlibm sin / cos / asin / acos (csrc/jfdlibm.h) evaluated on the device: the parity
+// self-check that device and host (oracle) results are bit-identical
+__global__ void math_eval_kernel(const double* __restrict__ x, double* __restrict__ out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double v = x[i];
+  out[4 * i + 0] = jf::sin(v);
+  out[4 * i + 1] = jf::cos(v);
+  out[4 * i + 2] = jf::asin(v);
+  out[4 * i + 3] = jf::acos(v);
 }
 
 extern "C" {
 
 int rt_render(rt_scene* s, const rt_render_params* p, float* rgb, int32_t* argb) { return render_host(s, p, rgb, argb, nullptr); }
+
+int rt_math_eval(const double* x, double* out, int64_t n, int device) {
+  if (n < 0 || (n > 0 && (!x || !out))) return set_error(RT_E_INVALID, "rt_math_eval: bad arguments");
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) return set_error(RT_E_NODEVICE, "no HIP device visible");
+  if (device < 0 || device >= nd) return set_error(RT_E_INVALID, "device ordinal out of range");
+  if (n == 0) return RT_OK;
+  HIPCHK(hipSetDevice(device));
+  double *dx = nullptr, *dout = nullptr;
+  HIPCHK(hipMalloc(&dx, sizeof(double) * n));
+  hipError_t e = hipMalloc(&dout, sizeof(double) * 4 * n);
+  if (e == hipSuccess) e = hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(math_eval_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dx, dout, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(double) * 4 * n, hipMemcpyDeviceToHost);
+  (void)hipFree(dx);
+  (void)hipFree(dout);
+  if (e != hipSuccess) return set_error(RT_E_HIP, hipGetErrorString(e));
+  return RT_OK;
+}
 
 int rt_render_count(rt_scene* s, const rt_render_params* p, float* rgb, int32_t* argb, uint64_t* stats) {
   if (!stats) return set_error(RT_E_INVALID, "null stats");

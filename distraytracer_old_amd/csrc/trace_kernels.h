@@ -13,6 +13,7 @@
 // and scratch use (hence occupancy) low for the common configurations.
 #pragma once
 #include "trace_device.h"
+#include "jfdlibm.h"  // sin / cos / asin / acos shared bit for bit with the oracle
 
 namespace rt {
 namespace dv {
@@ -856,13 +857,13 @@ DEVI V image_color(const SceneD& S, const HitRec& h, const Key& k, const TexD& T
     V to = sphere_center(P, k);
     double a0 = p.y - to.y, a1 = a0 / P.a[4];
     a1 = (a1 > 1) ? 1 : (a1 < -1) ? -1 : a1;
-    v = (T.h - 1) * acos(a1) / PI_D;
+    v = (T.h - 1) * jf::acos(a1) / PI_D;
     double shWm1 = T.w - 1, z1 = p.z - to.z, q = v / (T.h - 1);
     double b0 = (p.x - to.x) / P.a[3];
     b0 = (b0 > 1) ? 1 : (b0 < -1) ? -1 : b0;
-    double b1 = sin(q * PI_D);
+    double b1 = jf::sin(q * PI_D);
     double a2 = (fabs(b1) < EPS) ? 1 : b0 / b1;
-    u = (z1 <= EPS) ? ((shWm1 * acos(a2)) / TWO_PI_F + shWm1 / 2.0) : shWm1 - ((shWm1 * acos(a2)) / TWO_PI_F + shWm1 / 2.0);
+    u = (z1 <= EPS) ? ((shWm1 * jf::acos(a2)) / TWO_PI_F + shWm1 / 2.0) : shWm1 - ((shWm1 * jf::acos(a2)) / TWO_PI_F + shWm1 / 2.0);
     u = (u < 0) ? 0 : (u > shWm1) ? shWm1 : u;
   } else if (h.type == PT_TRI || h.type == PT_QUAD || h.type == PT_PLANE) {  // barycentric (myPlanarObject.java:178-186)
     double vx[4][3], uvv[4][2];
@@ -1053,7 +1054,7 @@ DEVI V diff_color(const SceneD& S, const MatD& m, const HitRec& h, const Key& k,
         }
         double lin = (hv.x * m.periodMult[0] + hv.y * m.periodMult[1] + hv.z * m.periodMult[2]);
         double spt = lin / m.pmMag + m.turbMult * res;
-        double dv = .5 * sin(spt) + .5;
+        double dv = .5 * jf::sin(spt) + .5;
         out = clr_ara(m, dv, hv);
       } else {  // wood: sqPtVal (myTextureHandler.java:275) + turbulence, banded by sin
         const double* pm = m.periodMult;
@@ -1070,7 +1071,7 @@ DEVI V diff_color(const SceneD& S, const MatD& m, const HitRec& h, const Key& k,
           }
         }
         const double sq = sqrt((hv.x * hv.x) * pm[0] + (hv.y * hv.y) * pm[1] + (hv.z * hv.z) * pm[2]) + m.turbMult * res;
-        double dv = sin(sq * m.pmMag);
+        double dv = jf::sin(sq * m.pmMag);
         if (m.tex == 3) {
           dv *= 1.1;
           dv += .5;
@@ -1470,13 +1471,13 @@ DEVI V background(const SceneD& S, const WRay& w, Counters& ct) {
       V p = mk(d.x * t + o.x, d.y * t + o.y, d.z * t + o.z);
       double a0 = p.y - c.y, a1 = a0 / r;
       a1 = (a1 > 1) ? 1 : (a1 < -1) ? -1 : a1;
-      double v = (T.h - 1) * acos(a1) / PI_D;
+      double v = (T.h - 1) * jf::acos(a1) / PI_D;
       double shWm1 = T.w - 1, z1 = (p.z - c.z), q = v / (T.h - 1);
       double b0 = (p.x - c.x) / r;
       b0 = (b0 > 1) ? 1 : (b0 < -1) ? -1 : b0;
-      double b1 = sin(q * PI_D);
+      double b1 = jf::sin(q * PI_D);
       double a2 = (fabs(b1) < EPS) ? 1 : b0 / b1;
-      double u = (z1 <= EPS) ? ((shWm1 * (acos(a2)) / (TWO_PI_F)) + shWm1 / 2.0) : shWm1 - ((shWm1 * (acos(a2)) / (TWO_PI_F)) + shWm1 / 2.0);
+      double u = (z1 <= EPS) ? ((shWm1 * (jf::acos(a2)) / (TWO_PI_F)) + shWm1 / 2.0) : shWm1 - ((shWm1 * (jf::acos(a2)) / (TWO_PI_F)) + shWm1 / 2.0);
       u = (u < 0) ? 0 : (u > shWm1) ? shWm1 : u;
       if (CNT) ct.c[C_TEXEL]++;
       return texel(S, T, (long)jd2i(v) * T.w + jd2i(u));
@@ -1486,7 +1487,7 @@ DEVI V background(const SceneD& S, const WRay& w, Counters& ct) {
 }
 
 DEVI V rot_axis(V v1, V u, double thet) {  // rotVecAroundAxis (DistRayTracer.java:336-349)
-  double cT = cos(thet), sT = sin(thet), oneMC = 1 - cT, ux2 = u.x * u.x, uy2 = u.y * u.y, uz2 = u.z * u.z,
+  double cT = jf::cos(thet), sT = jf::sin(thet), oneMC = 1 - cT, ux2 = u.x * u.x, uy2 = u.y * u.y, uz2 = u.z * u.z,
          uxy = u.x * u.y, uxz = u.x * u.z, uyz = u.y * u.z, uzS = u.z * sT, uyS = u.y * sT, uxS = u.x * sT,
          uxzC1 = uxz * oneMC, uxyC1 = uxy * oneMC, uyzC1 = uyz * oneMC;
   return mk((ux2 * oneMC + cT) * v1.x + (uxyC1 - uzS) * v1.y + (uxzC1 + uyS) * v1.z,
@@ -1543,7 +1544,7 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     double ltMult = 1;
     if (CNT) ct.c[C_LIGHT]++;
     if ((F & FT_LIGHTX) && ltype == 1) {  // mySpotLight.intersectCheck / calcT_Mult (myLight.java:77-82,159-163)
-      double angle = acos(-1 * dot(sr.d, ld3(L.orient)));
+      double angle = jf::acos(-1 * dot(sr.d, ld3(L.orient)));
       ltMult = (angle < L.innerRad) ? 1 : (angle > L.outerRad) ? 0 : (L.outerRad - angle) / L.radDiff;
     }
     if (ltMult == 0) continue;
@@ -1603,12 +1604,12 @@ DEVI TransOut trans_split(const MatD& m, const HitRec& h, const double* inKt, bo
   if (cos1 < EPS) { rnm = -1.0; N = mk(N.x * -1, N.y * -1, N.z * -1); }
   cos1 = dot(back, N);
   double mb = mag(back), mn = mag(N);
-  double thetaI = acos(dot(back, N) / (mb * mn));  // _angleBetween (DistRayTracer.java:445-452)
+  double thetaI = jf::acos(dot(back, N) / (mb * mn));  // _angleBetween (DistRayTracer.java:445-452)
   double idx = strans ? m.perm : m.ktrans;
   double n = 1, n1 = 0, n2 = 0, cos2 = 0, tr = 0, omtr = 1;
   bool TIR = false;
   if (rnm < 0) {  // leaving the material
-    double thetaCrit = asin(1.0 / idx);
+    double thetaCrit = jf::asin(1.0 / idx);
     if (thetaI < thetaCrit) {
       n1 = idx; n2 = 1; n = (n1 / n2);
       cos2 = sqrt(1.0 - (n * n) * (1.0 - (cos1 * cos1)));
@@ -1622,7 +1623,7 @@ DEVI TransOut trans_split(const MatD& m, const HitRec& h, const double* inKt, bo
     cos2 = sqrt(1.0 - (n * n) * (1.0 - (cos1 * cos1)));
   }
   if (!TIR) {  // Fresnel with cos(theta_t) = sqrt(1 - (n1/n2) sin^2) (Q15)
-    double sa = sin(acos(cos1)), rct = sqrt(1.0 - ((n1 / n2) * sa * sa));
+    double sa = jf::sin(jf::acos(cos1)), rct = sqrt(1.0 - ((n1 / n2) * sa * sa));
     double a1 = n1 * cos1, b1 = n2 * rct, nd1 = (a1 - b1) / (a1 + b1);
     double a2 = n1 * rct, b2 = n2 * cos1, nd2 = (a2 - b2) / (a2 + b2);
     tr = ((nd1 * nd1) + (nd2 * nd2)) / 2.0;
@@ -1933,9 +1934,9 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
           rSq = yVal * yVal + xVal * xVal;
           traced = rSq <= 1;
         }
-        const double r = sqrt(rSq), theta = r * P.aperHalf, phi = atan2(-yVal, xVal), sTh = sin(theta);
+        const double r = sqrt(rSq), theta = r * P.aperHalf, phi = atan2(-yVal, xVal), sTh = jf::sin(theta);
         o = mk(0, 0, 0);
-        d = mk(sTh * cos(phi), sTh * sin(phi), -cos(theta));
+        d = mk(sTh * jf::cos(phi), sTh * jf::sin(phi), -jf::cos(theta));
       } else if ((F & FT_CAMX) && P.cam == 2) {  // myOrthoScene: draw :1704-1745 / shootMultiRays :1690-1702
         const double rayYOffset = P.H / 2.0, rayXOffset = P.W / 2.0;
         double rx, ry;

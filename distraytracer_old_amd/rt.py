@@ -42,7 +42,7 @@ EXPORTS = ["rt_abi_version", "rt_last_error", "rt_device_count", "rt_scene_creat
            "rt_render_count", "rt_time_render", "rt_render_pass", "rt_refine_steps", "rt_scene_photons",
            "rt_scene_photon_map", "rt_photons_shoot",
            "rt_photons_set",
-           "rt_png_name", "rt_scene_save_name"]
+           "rt_png_name", "rt_scene_save_name", "rt_math_eval"]
 
 _lib = None
 
@@ -89,6 +89,7 @@ def lib():
                                        ctypes.c_void_p, ctypes.c_void_p]
         L.rt_time_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_double)]
+        L.rt_math_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
         L.rt_png_name.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
         L.rt_scene_save_name.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
         _lib = L
@@ -112,6 +113,14 @@ def png_name(save_name: str) -> str:
 def _check(rc: int, what: str):
     if rc != 0:
         raise RTError(f"{what} failed ({rc}): {lib().rt_last_error().decode()}")
+
+
+def math_eval(x, device: int = 0) -> np.ndarray:
+    """Device fdlibm sin / cos / asin / acos of x (diagnostics, rt_math_eval): [n, 4] float64."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.zeros((len(x), 4), dtype=np.float64)
+    _check(lib().rt_math_eval(x.ctypes.data, out.ctypes.data, len(x), device), "rt_math_eval")
+    return out
 
 
 def device_count() -> int:

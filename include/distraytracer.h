@@ -231,7 +231,8 @@ int rt_photons_shoot(rt_scene* scene, uint64_t seed, int64_t first, int64_t coun
 /* Set the photon_list (insertion order) and build / upload the photon map from it. */
 int rt_photons_set(rt_scene* scene, const double* pos, const double* pwr, int64_t n);
 
-/* Blocking render into caller-owned HOST buffers (either may be NULL).
+/* Blocking render into caller-owned HOST buffers (either may be NULL). Runs on the scene's own
+   stream with device output buffers kept across calls (no per-call allocation or device-wide sync).
    rgb: float[n_rows*width*3] clamped <=1 per myColor; argb: int32[n_rows*width], reference packing. */
 int rt_render(rt_scene* scene, const rt_render_params* p, float* rgb, int32_t* argb);
 /* Asynchronous render into caller-owned DEVICE buffers on `hip_stream` (hipStream_t, may be NULL).
@@ -255,6 +256,10 @@ int rt_render_count(rt_scene* scene, const rt_render_params* p, float* rgb, int3
 /* Kernel-only timing helper: average ms of the render kernel over `iters` launches (HIP events on the
    launch stream), inputs resident in HBM; at least 2 warmup launches (the schedule calibration). */
 int rt_time_render(rt_scene* scene, const rt_render_params* p, int warmup, int iters, double* avg_ms);
+
+/* Diagnostics: the device's fdlibm sin / cos / asin / acos (the sequences the trace kernels use,
+   shared bit for bit with the CPU oracle) of x[0..n) into out[4*i .. 4*i+3], host buffers. */
+int rt_math_eval(const double* x, double* out, int64_t n, int device);
 
 #ifdef __cplusplus
 }

@@ -31,7 +31,8 @@ def build(force: bool = False) -> Path:
     source is newer than the library; on the GPU box (no compiler run wanted) a present library
     is used as shipped."""
     src_newer = LIB_PATH.exists() and any(
-        f.stat().st_mtime > LIB_PATH.stat().st_mtime for f in (ORACLE_DIR / "src").iterdir())
+        f.stat().st_mtime > LIB_PATH.stat().st_mtime
+        for f in [*(ORACLE_DIR / "src").iterdir(), ORACLE_DIR.parent / "distraytracer_old_amd" / "csrc" / "jfdlibm.h"])
     if force or not LIB_PATH.exists() or src_newer:
         subprocess.run(["make", "-C", str(ORACLE_DIR)] + (["-B"] if force else []), check=True, capture_output=True)
     return LIB_PATH
@@ -53,9 +54,19 @@ def lib():
         L.oracle_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_int]
+        L.oracle_set_photons.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+        L.oracle_math_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         L.oracle_camera_hits.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         _lib = L
     return _lib
+
+
+def math_eval(x) -> np.ndarray:
+    """Host fdlibm sin / cos / asin / acos (the oracle's, csrc/jfdlibm.h): [n, 4] float64."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.zeros((len(x), 4), dtype=np.float64)
+    lib().oracle_math_eval(x.ctypes.data, out.ctypes.data, len(x))
+    return out
 
 
 class OracleScene:
@@ -78,6 +89,12 @@ class OracleScene:
 
     def build_photons(self, seed: int) -> int:
         return lib().oracle_build_photons(self._h, seed)
+
+    def set_photons(self, pos, pwr):
+        """Install a photon_list (insertion order) and build the oracle's kd-tree over it."""
+        pos = np.ascontiguousarray(pos, dtype=np.float64)
+        pwr = np.ascontiguousarray(pwr, dtype=np.float64)
+        lib().oracle_set_photons(self._h, pos.ctypes.data, pwr.ctypes.data, len(pos))
 
     def photons(self):
         """(pos [n,3], pwr [n,3]) of the photon map in insertion order (after build_photons)."""

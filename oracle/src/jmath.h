@@ -18,6 +18,10 @@
 #include <cstring>
 #include <limits>
 
+// sin / cos / asin / acos: fdlibm (java.lang.StrictMath's algorithms), the same operation sequences
+// the device evaluates (one header for both sides: results bit-identical)
+#include "../../distraytracer_old_amd/csrc/jfdlibm.h"
+
 namespace orc {
 
 static const double EPS = 0.0000001;                       // DistRayTracer.java:53
@@ -194,7 +198,7 @@ static inline CTM build_ctm(const M4& g) {
 }
 
 static inline V3 rot_around_axis(const V3& v1, const V3& u, double thet) {
-  double cT = std::cos(thet), sT = std::sin(thet), oneMC = 1 - cT, ux2 = u.x * u.x, uy2 = u.y * u.y,
+  double cT = jf::cos(thet), sT = jf::sin(thet), oneMC = 1 - cT, ux2 = u.x * u.x, uy2 = u.y * u.y,
          uz2 = u.z * u.z, uxy = u.x * u.y, uxz = u.x * u.z, uyz = u.y * u.z, uzS = u.z * sT, uyS = u.y * sT,
          uxS = u.x * sT, uxzC1 = uxz * oneMC, uxyC1 = uxy * oneMC, uyzC1 = uyz * oneMC;
   return V3((ux2 * oneMC + cT) * v1.x + (uxyC1 - uzS) * v1.y + (uxzC1 + uyS) * v1.z,

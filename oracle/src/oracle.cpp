@@ -423,13 +423,13 @@ struct Sphere : SceneObject {
     V3 to = getOrigin(time);
     double a0 = p.y - to.y, a1 = a0 / radY;
     a1 = (a1 > 1) ? 1 : (a1 < -1) ? -1 : a1;
-    v = (tex.h - 1) * std::acos(a1) / M_PI;
+    v = (tex.h - 1) * jf::acos(a1) / M_PI;
     double shWm1 = tex.w - 1, z1 = p.z - to.z, q = v / (tex.h - 1);
     double b0 = (p.x - to.x) / radX;
     b0 = (b0 > 1) ? 1 : (b0 < -1) ? -1 : b0;
-    double b1 = std::sin(q * M_PI);
+    double b1 = jf::sin(q * M_PI);
     double a2 = (std::fabs(b1) < EPS) ? 1 : b0 / b1;
-    u = (z1 <= EPS) ? ((shWm1 * std::acos(a2)) / TWO_PI_F + shWm1 / 2.0) : shWm1 - ((shWm1 * std::acos(a2)) / TWO_PI_F + shWm1 / 2.0);
+    u = (z1 <= EPS) ? ((shWm1 * jf::acos(a2)) / TWO_PI_F + shWm1 / 2.0) : shWm1 - ((shWm1 * jf::acos(a2)) / TWO_PI_F + shWm1 / 2.0);
     u = (u < 0) ? 0 : (u > shWm1) ? shWm1 : u;
   }
 };
@@ -968,13 +968,13 @@ static Color background(Scene* s, Ray& ray, uint64_t* st) {
   V3 p = ray.point(t);
   double a0 = p.y - sd->origin.y, a1 = a0 / (sd->radY);
   a1 = (a1 > 1) ? 1 : (a1 < -1) ? -1 : a1;
-  double v = (tex.h - 1) * std::acos(a1) / M_PI;
+  double v = (tex.h - 1) * jf::acos(a1) / M_PI;
   double shWm1 = tex.w - 1, z1 = (p.z - sd->origin.z), q = v / (tex.h - 1);
   double b0 = (p.x - sd->origin.x) / (sd->radX);
   b0 = (b0 > 1) ? 1 : (b0 < -1) ? -1 : b0;
-  double b1 = std::sin(q * M_PI);
+  double b1 = jf::sin(q * M_PI);
   double a2 = (std::fabs(b1) < EPS) ? 1 : b0 / b1;
-  double u = (z1 <= EPS) ? ((shWm1 * (std::acos(a2)) / (TWO_PI_F)) + shWm1 / 2.0) : shWm1 - ((shWm1 * (std::acos(a2)) / (TWO_PI_F)) + shWm1 / 2.0);
+  double u = (z1 <= EPS) ? ((shWm1 * (jf::acos(a2)) / (TWO_PI_F)) + shWm1 / 2.0) : shWm1 - ((shWm1 * (jf::acos(a2)) / (TWO_PI_F)) + shWm1 / 2.0);
   u = (u < 0) ? 0 : (u > shWm1) ? shWm1 : u;
   if (st) st[ST_TEXEL]++;
   long idx = (long)jd2i(v) * tex.w + jd2i(u);
@@ -1172,7 +1172,7 @@ static void diff_txtr_color(Shader* sh, Hit& hit, double diffConst, double out[3
       hv = V3(hv.x * sh->scale, hv.y * sh->scale, hv.z * sh->scale);
       double res = noise3((float)hv.x, (float)hv.y, (float)hv.z);
       double sq = std::sqrt((hv.x * hv.x) * pm.x + (hv.y * hv.y) * pm.y + (hv.z * hv.z) * pm.z) + sh->turbMult * res;
-      double distVal = std::sin(sq * mag(pm));
+      double distVal = jf::sin(sq * mag(pm));
       distVal *= 1.1;
       distVal += .5;
       distVal = (distVal < 0 ? 0 : (distVal > 1 ? 1 : distVal));
@@ -1186,7 +1186,7 @@ static void diff_txtr_color(Shader* sh, Hit& hit, double diffConst, double out[3
         fs *= 1.92;
       }
       double sq = std::sqrt((hv.x * hv.x) * pm.x + (hv.y * hv.y) * pm.y + (hv.z * hv.z) * pm.z) + sh->turbMult * res;
-      double distVal = (std::sin(sq * mag(pm)));
+      double distVal = (jf::sin(sq * mag(pm)));
       distVal = 1 - (distVal < 0 ? 0 : distVal);
       clr_ara(sh, distVal, hv, out);
     } else if (sh->tex == TX_NOISE) {  // myNoiseTexture :257-265
@@ -1204,7 +1204,7 @@ static void diff_txtr_color(Shader* sh, Hit& hit, double diffConst, double out[3
       }
       double lin = (hv.x * sh->periodMult.x + hv.y * sh->periodMult.y + hv.z * sh->periodMult.z);
       double spt = lin / mag(sh->periodMult) + sh->turbMult * res;
-      double distVal = .5 * std::sin(spt) + .5;
+      double distVal = .5 * jf::sin(spt) + .5;
       clr_ara(sh, distVal, hv, out);
     }
     if (std::fabs(diffConst - 1.0) > EPS) { out[0] *= diffConst; out[1] *= diffConst; out[2] *= diffConst; }
@@ -1233,7 +1233,7 @@ static void shadow_color(Scene* s, Shader* sh, Hit& hit, const double tex[3], do
     double ltMult = 1;
     if (st) st[ST_LIGHT]++;
     if (L->ltype == LT_SPOT) {
-      double angle = std::acos(-1 * dot(sr.direction, L->orientation));
+      double angle = jf::acos(-1 * dot(sr.direction, L->orientation));
       ltMult = L->angle_prob(angle);
     }
     if (ltMult == 0) continue;
@@ -1271,7 +1271,7 @@ static V3 refl_dir(const V3& eye, const V3& n) {  // compReflDir :89-96
 }
 static double angle_between(const V3& v1, const V3& v2) {  // DistRayTracer.java:445-452
   double m1 = mag(v1), m2 = mag(v2), dp = dot(v1, v2), ca = dp / (m1 * m2);
-  return std::acos(ca);
+  return jf::acos(ca);
 }
 static double fres_perp(double n1, double n2, double ci, double ct) { double a = n1 * ci, b = n2 * ct, nd = (a - b) / (a + b); return nd * nd; }
 static double fres_plel(double n1, double n2, double ci, double ct) { double a = n1 * ct, b = n2 * ci, nd = (a - b) / (a + b); return nd * nd; }
@@ -1295,7 +1295,7 @@ static TransSplit trans_split(const Shader* sh, const Hit& hit, bool simple) {
   double idx = simple ? sh->currPerm : sh->KTrans;
   if (simple) S.reflDir = refl_dir(S.back, S.N);
   if (S.refractNormMult < 0) {
-    double thetaCrit = std::asin(exitT / idx);
+    double thetaCrit = jf::asin(exitT / idx);
     if (thetaI < thetaCrit) {
       S.n1 = idx; S.n2 = exitT; S.n = (S.n1 / S.n2);
       double c2 = 1.0 - (S.n * S.n) * (1.0 - (cos1 * cos1));
@@ -1311,7 +1311,7 @@ static TransSplit trans_split(const Shader* sh, const Hit& hit, bool simple) {
     S.cos2 = std::sqrt(c2);
   }
   if (!S.TIR) {
-    double sa = std::sin(std::acos(cos1)), rct = std::sqrt(1.0 - ((S.n1 / S.n2) * sa * sa));
+    double sa = jf::sin(jf::acos(cos1)), rct = std::sqrt(1.0 - ((S.n1 / S.n2) * sa * sa));
     double rp = fres_perp(S.n1, S.n2, cos1, rct), rl = fres_plel(S.n1, S.n2, cos1, rct);
     S.tr = (rp + rl) / 2.0;
     S.omtr = 1 - S.tr;
@@ -1737,7 +1737,7 @@ struct Loader {
     R1.m[1][0] = bv.x; R1.m[1][1] = bv.y; R1.m[1][2] = bv.z;
     R1.m[2][0] = cv.x; R1.m[2][1] = cv.y; R1.m[2][2] = cv.z;
     M4 R1T = transpose(R1);
-    R2.m[1][1] = std::cos(ar); R2.m[1][2] = -std::sin(ar); R2.m[2][1] = std::sin(ar); R2.m[2][2] = std::cos(ar);
+    R2.m[1][1] = jf::cos(ar); R2.m[1][2] = -jf::sin(ar); R2.m[2][1] = jf::sin(ar); R2.m[2][2] = jf::cos(ar);
     M4 tmp = mmul(R2, R1);
     stack.back() = mmul(stack.back(), mmul(R1T, tmp));
   }
@@ -2280,8 +2280,8 @@ int oracle_render(void* p, int W, int H, int spp, uint64_t seed, int row0, int r
         const double fishMult = 2.0 / maxDim;  // setImageSize :780-792
         const double aperatureHlf = (M_PI * s->fishEye / 180.0) / 2.0;
         auto fish_ray = [&](double xVal, double yVal, double rSq, uint32_t k) -> Color {
-          double r = std::sqrt(rSq), theta = r * aperatureHlf, phi = std::atan2(-yVal, xVal), sTh = std::sin(theta);
-          Ray ray(V3(0, 0, 0), V3(sTh * std::cos(phi), sTh * std::sin(phi), -std::cos(theta)), 0);
+          double r = std::sqrt(rSq), theta = r * aperatureHlf, phi = std::atan2(-yVal, xVal), sTh = jf::sin(theta);
+          Ray ray(V3(0, 0, 0), V3(sTh * jf::cos(phi), sTh * jf::sin(phi), -jf::cos(theta)), 0);
           ray.key.seed = seed; ray.key.pixel = pix; ray.key.sample = k; ray.key.node = 1;
           st[ST_CAM]++;
           return reflect_ray(s, ray, st);
@@ -2372,6 +2372,29 @@ int oracle_render(void* p, int W, int H, int spp, uint64_t seed, int row0, int r
   if (stats)
     for (auto& v : tst)
       for (int i = 0; i < ST_N; ++i) stats[i] += v[i];
+  return 0;
+}
+
+// Install a photon_list (insertion order; e.g. the product's rt_scene_photons output) and build
+// the oracle's own kd-tree over it (myKD_Tree.build_tree, myLight.java:325-381), so both sides
+// gather over the identical list (tests/test_gpu_parity.py C5 at k = 200).
+int oracle_set_photons(void* p, const double* pos, const double* pwr, int64_t n) {
+  Scene* s = (Scene*)p;
+  KDTree& T = s->photonTree;
+  T.photons.assign((size_t)n, Photon{});
+  for (int64_t i = 0; i < n; ++i)
+    for (int c = 0; c < 3; ++c) { T.photons[i].pos[c] = pos[3 * i + c]; T.photons[i].pwr[c] = pwr[3 * i + c]; }
+  T.build_all();
+  s->photonsBuilt = true;
+  return 0;
+}
+
+// fdlibm sin / cos / asin / acos (jfdlibm.h, shared with the device) of x[0..n) -> out[4*i..4*i+3]
+int oracle_math_eval(const double* x, double* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) {
+    out[4 * i + 0] = jf::sin(x[i]); out[4 * i + 1] = jf::cos(x[i]);
+    out[4 * i + 2] = jf::asin(x[i]); out[4 * i + 3] = jf::acos(x[i]);
+  }
   return 0;
 }
 
