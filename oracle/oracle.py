@@ -39,10 +39,13 @@ def build(force: bool = False) -> Path:
 
 
 def lib():
+    """ORACLE_LIB overrides the library (the sanitizer build, tools/sanitize.sh)."""
     global _lib
     if _lib is None:
-        build()
-        L = ctypes.CDLL(str(LIB_PATH))
+        path = os.environ.get("ORACLE_LIB")
+        if not path:
+            build()
+        L = ctypes.CDLL(path or str(LIB_PATH))
         L.oracle_last_error.restype = ctypes.c_char_p
         L.oracle_register_texture.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.oracle_load.restype = ctypes.c_void_p
