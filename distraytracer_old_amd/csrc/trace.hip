@@ -323,6 +323,7 @@ static uint32_t scene_features(const HostScene& h) {
   if (h.camera != RT_CAMERA_FOV) f |= dv::FT_CAMX;
   for (const MatD& m : h.mat) {
     if (m.tex != 0) f |= dv::FT_TEX;
+    if (m.tex == 5) f |= dv::FT_CELL;
     if (m.usePhotonMap) f |= dv::FT_PHOTON;
     if (m.ktrans > 0 || m.perm > 0.0) f |= dv::FT_TRANS;
   }

@@ -29,7 +29,8 @@ enum : uint32_t {
   FT_CAMX = 64,   // fisheye or orthographic camera
   FT_INST = 128,  // instances (named_object / instance / sierpinski)
   FT_PASS = 256,  // column step of a `refine` pass (rt_render_pass; never a scene feature)
-  FT_ALL = 511
+  FT_CELL = 512,  // cellular `stone` textures (myCellularTexture: per-cell LCG, pow / log ROI functions)
+  FT_ALL = 1023
 };
 
 __constant__ int c_perm[256];
@@ -1027,12 +1028,16 @@ DEVI V cellular_color(const MatD& m, const HitRec& h) {
 // getDiffTxtrColor of the shader's texture handler (myTextureHandler.java)
 template <bool CNT, uint32_t F>
 DEVI V diff_color(const SceneD& S, const MatD& m, const HitRec& h, const Key& k, double diffConst, Counters& ct) {
+#ifdef RT_PROF_NOTEX  // profiling builds only (tools/variant_sweep.py): results differ
+  if constexpr (false) {
+#else
   if constexpr ((F & FT_TEX) != 0) {
+#endif
     if (m.tex == 1) {  // myImageTexture :105-117
       V c = (m.texTop >= 0) ? image_color<CNT>(S, h, k, S.tex[m.texTop], ct) : ld3(m.diffuse);
       return mk(c.x * diffConst, c.y * diffConst, c.z * diffConst);
     }
-    if (m.tex == 5) {
+    if ((F & FT_CELL) && m.tex == 5) {
       V out = cellular_color(m, h);
       if (fabs(diffConst - 1.0) > EPS) out = mk(out.x * diffConst, out.y * diffConst, out.z * diffConst);
       return out;
@@ -1646,19 +1651,34 @@ DEVI TransOut trans_split(const MatD& m, const HitRec& h, const double* inKt, bo
 // shading tree. A node spawns child A at once; a frame keeps what the node
 // needs when its children return: local colour, accumulated child sum,
 // weights, and (two-child nodes only) the second child's ray.
+//
+// The ray's medium (myRay.currKTrans, myRay.java:26-47) is a material index: the reference
+// copies {KTrans, perm, permClr} of the material that spawned a refracted ray, or all 1s
+// (camera / reflected rays, the simple shader's reflection), and reads only entries 0 and 1
+// (calcTransClr n1, myObjShader.java:193; calcSimpleTransClr :525).
 struct Child {  // outgoing ray
   V o, d;
-  double kt[5];
+  int32_t ktm;  // medium: material whose (ktrans, perm) are currKTrans[0..1]; -1 = all 1s
   uint32_t node;
   int32_t gen;
 };
+DEVI void kt_of(const SceneD& S, int32_t ktm, double ik[2]) {
+  if (ktm < 0) { ik[0] = 1; ik[1] = 1; }
+  else { ik[0] = S.mat[ktm].ktrans; ik[1] = S.mat[ktm].perm; }
+}
+// Transparent variants: weights are rebuilt from the material at the child's return with
+// the same products the reference forms (omtr * permClr, tr * kRefl, ...), so a frame holds
+// two scalars instead of two colours; the B child's medium is the material again.
+// Only the fields a node's case needs are written (the frame stack lives in scratch).
+enum : uint8_t { FM_REFL = 0, FM_FRESNEL = 1, FM_SIMPLE = 2 };  // weight rule of a frame
 template <uint32_t F>
 struct FrameT {
-  V local, acc, wA, wB, org, dB;
-  double ktB[5];
+  V local, acc, org, dB;  // acc: child A's weighted colour, kept only while B is traced
+  double wa, wb;          // FM_FRESNEL / FM_SIMPLE: omtr, tr of the split
+  int32_t mat;
   uint32_t node;
   int32_t gen;
-  uint8_t phase, hasB, kindB;  // kindB: counter class of child B
+  uint8_t phase, hasB, mode;  // phase 1: A out; 2: B out after A; 3: B out, no A
 };
 template <uint32_t F>
 struct FrameR {  // no transparent materials: at most one child (reflection), weight = mat.kreflclr
@@ -1691,7 +1711,6 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
   V ls = light_sum<CNT, F>(S, m, h, tex, k, ct);
   r += ls.x; g += ls.y; b += ls.z;
   Fr.local = mk(r, g, b);
-  if constexpr ((F & FT_TRANS) != 0) Fr.acc = mk(0, 0, 0);
   branch = (in.gen < S.numRays - 2) && m.hasCaustic;
 #ifdef RT_PROF_NOSECONDARY  // profiling builds only: results differ
   branch = false;
@@ -1704,36 +1723,35 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
     bool trans = !m.simple && ((m.ktrans > 0) || (m.perm > 0.0));
     bool strans = m.simple && (m.ktrans > 0);
     if (trans || strans) {  // calcTransClr :157-276 / calcSimpleTransClr :503-631
-      TransOut T = trans_split(m, h, in.kt, strans);
-      double kt[5] = {m.ktrans, m.perm, m.permclr[0], m.permclr[1], m.permclr[2]};
-      Fr.hasB = 0;
-      Fr.org = h.fwd;
-      Fr.node = in.node;
-      Fr.gen = in.gen;
-      if (T.doB) {
-        Fr.dB = T.refl;
-        Fr.hasB = 1;
-        Fr.kindB = C_REFL;
-        for (int i = 0; i < 5; ++i) Fr.ktB[i] = strans ? 1.0 : kt[i];
-        if (strans) { double w = T.tr * m.krefl; Fr.wB = mk(w, w, w); }
-        else Fr.wB = mk((T.tr) * m.permclr[0], (T.tr) * m.permclr[1], (T.tr) * m.permclr[2]);
-      }
+      double ik[2];
+      kt_of(S, in.ktm, ik);
+      const TransOut T = trans_split(m, h, ik, strans);
+      // children's medium: the material's {KTrans, perm, permClr}; the simple shader's
+      // reflection child gets all 1s
+      Fr.mat = h.mat;
+      Fr.mode = strans ? FM_SIMPLE : FM_FRESNEL;
+      Fr.wa = T.omtr;
+      Fr.wb = T.tr;
       if (T.doA) {
         a.d = T.refr;
-        for (int i = 0; i < 5; ++i) a.kt[i] = kt[i];
-        if (strans) { double w = T.omtr * m.ktrans; Fr.wA = mk(w, w, w); }
-        else Fr.wA = mk((T.omtr) * m.permclr[0], (T.omtr) * m.permclr[1], (T.omtr) * m.permclr[2]);
+        a.ktm = h.mat;
         if (CNT) ct.c[C_REFR]++;
         Fr.phase = 1;
-        return Fr.hasB ? 2 : 1;
+        Fr.hasB = T.doB;
+        if (T.doB) {
+          Fr.dB = T.refl;
+          Fr.org = h.fwd;
+          Fr.node = in.node;
+          Fr.gen = in.gen;
+        }
+        return T.doB ? 2 : 1;
       }
-      if (Fr.hasB) {  // only the reflection child: spawn it as "B"
-        a.d = Fr.dB;
+      if (T.doB) {  // only the reflection child: spawn it as "B"
+        a.d = T.refl;
         a.node = in.node * 2 + 1;
-        for (int i = 0; i < 5; ++i) a.kt[i] = Fr.ktB[i];
+        a.ktm = strans ? -1 : h.mat;
         if (CNT) ct.c[C_REFL]++;
-        Fr.phase = 2;
-        Fr.hasB = 0;
+        Fr.phase = 3;
         return 1;
       }
       return 0;
@@ -1744,13 +1762,12 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
     V rd = refl_dir(back, h.nrm);
     if (dot(rd, h.nrm) >= 0) {
       a.d = rd;
-      for (int i = 0; i < 5; ++i) a.kt[i] = 1;
+      a.ktm = -1;
       Fr.phase = 1;
+      Fr.mat = h.mat;
       if constexpr ((F & FT_TRANS) != 0) {
-        Fr.wA = mk(m.kreflclr[0], m.kreflclr[1], m.kreflclr[2]);
+        Fr.mode = FM_REFL;
         Fr.hasB = 0;
-      } else {
-        Fr.mat = h.mat;
       }
       if (CNT) ct.c[C_REFL]++;
       return 1;
@@ -1769,8 +1786,7 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
   FrameOf<F> fr[MAX_FRAMES];
   int sp = 0;
   Child in;
-  in.o = org; in.d = dir; in.node = 1; in.gen = 0;
-  for (int i = 0; i < 5; ++i) in.kt[i] = 1;
+  in.o = org; in.d = dir; in.node = 1; in.gen = 0; in.ktm = -1;
   while (true) {
     V c;
     {
@@ -1813,20 +1829,33 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
         c = clampc(add(P.local, acc));
         sp--;
       } else {
-        if (P.phase == 1) {
-          P.acc = mk(P.acc.x + (P.wA.x * c.x), P.acc.y + (P.wA.y * c.y), P.acc.z + (P.wA.z * c.z));
+        // the weights of the reference's frame, rebuilt from the material (same products)
+        const MatD& m = S.mat[P.mat];
+        const uint8_t ph = P.phase, mode = P.mode;
+        V acc;
+        if (ph == 1) {
+          V wA;
+          if (mode == FM_REFL) wA = mk(m.kreflclr[0], m.kreflclr[1], m.kreflclr[2]);
+          else if (mode == FM_SIMPLE) { const double w = P.wa * m.ktrans; wA = mk(w, w, w); }
+          else wA = mk(P.wa * m.permclr[0], P.wa * m.permclr[1], P.wa * m.permclr[2]);
+          acc = mk(0 + (wA.x * c.x), 0 + (wA.y * c.y), 0 + (wA.z * c.z));
           if (P.hasB) {  // second child (Fresnel reflection)
             P.phase = 2;
+            P.acc = acc;
             in.o = P.org; in.d = P.dB; in.gen = P.gen + 1; in.node = P.node * 2 + 1;
-            for (int i = 0; i < 5; ++i) in.kt[i] = P.ktB[i];
+            in.ktm = (mode == FM_SIMPLE) ? -1 : P.mat;
             if (CNT) ct.c[C_REFL]++;
             spawned = true;
             break;
           }
         } else {
-          P.acc = mk(P.acc.x + (P.wB.x * c.x), P.acc.y + (P.wB.y * c.y), P.acc.z + (P.wB.z * c.z));
+          V wB;
+          if (mode == FM_SIMPLE) { const double w = P.wb * m.krefl; wB = mk(w, w, w); }
+          else wB = mk(P.wb * m.permclr[0], P.wb * m.permclr[1], P.wb * m.permclr[2]);
+          const V a0 = (ph == 2) ? P.acc : mk(0, 0, 0);
+          acc = mk(a0.x + (wB.x * c.x), a0.y + (wB.y * c.y), a0.z + (wB.z * c.z));
         }
-        c = clampc(add(P.local, P.acc));
+        c = clampc(add(P.local, acc));
         sp--;
       }
     }
@@ -1911,8 +1940,8 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
     double t = -(dot(fN, fo) + S.lensFocal) / pr;
     fpt = mk(fd.x * t + fo.x, fd.y * t + fo.y, fd.z * t + fo.z);
   }
+  // per-pixel sums; the 1-spp non-DOF path (no averaging) keeps its one colour here instead
   double rs = 0, gs = 0, bs = 0;
-  V c1 = mk(0, 0, 0);
   for (int s0 = 0; s0 < n; s0 += G) {
     const int s = s0 + j;
     V cc = mk(0, 0, 0);
@@ -1974,8 +2003,8 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
       }
     }
     if (G == 1) {
-      c1 = cc;
-      if (traced) { rs += cc.x; gs += cc.y; bs += cc.z; }
+      if (n == 1 && !dof) { rs = cc.x; gs = cc.y; bs = cc.z; }
+      else if (traced) { rs += cc.x; gs += cc.y; bs += cc.z; }
     } else {
       cbuf[4 * lane + 0] = cc.x;
       cbuf[4 * lane + 1] = cc.y;
@@ -1993,7 +2022,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
     }
   }
   if (valid && j == 0) {
-    V c = (n == 1 && !dof) ? c1 : clampc(mk(rs / n, gs / n, bs / n));
+    V c = (n == 1 && !dof) ? mk(rs, gs, bs) : clampc(mk(rs / n, gs / n, bs / n));
     const size_t o = (size_t)ri * ncols + ci;
     if (rgb) {
       rgb[3 * o + 0] = (float)c.x;
@@ -2102,21 +2131,23 @@ DEVI void photon_ray(const LightD& L, uint64_t seed, uint64_t i, V& o, V& d) {
   o = xpt(L.g, disk_pos(L, kk, 0));
 }
 // findCausticRayHit (myObjShader.java:461-478) with calcTransRay / calcReflRay
-DEVI bool caustic_ray(const SceneD& S, const HitRec& h, const double* inKt, int gen, double pwr[3], Child& out) {
+DEVI bool caustic_ray(const SceneD& S, const HitRec& h, int32_t inKtm, int gen, double pwr[3], Child& out) {
   const MatD& m = S.mat[h.mat];
   if (!((gen < 4) && m.hasCaustic)) return false;  // numPhotonRays = 4
   double pmul[3] = {1.0, 1.0, 1.0};
   bool ok = false;
   if ((m.ktrans > 0.0) || (m.perm > 0.0)) {
     pmul[0] = m.phtnPermClr[0]; pmul[1] = m.phtnPermClr[1]; pmul[2] = m.phtnPermClr[2];
-    TransOut T = trans_split(m, h, inKt, false);
+    double ik[2];
+    kt_of(S, inKtm, ik);
+    TransOut T = trans_split(m, h, ik, false);
     out.d = (T.omtr > EPS) ? T.refr : T.refl;
-    out.kt[0] = m.ktrans; out.kt[1] = m.perm; out.kt[2] = m.permclr[0]; out.kt[3] = m.permclr[1]; out.kt[4] = m.permclr[2];
+    out.ktm = h.mat;
     ok = true;
   } else if (m.krefl > 0.0) {
     pmul[0] = pmul[1] = pmul[2] = m.krefl;
     out.d = refl_dir(mk(h.dw.x * -1, h.dw.y * -1, h.dw.z * -1), h.nrm);
-    for (int c = 0; c < 5; ++c) out.kt[c] = 1;
+    out.ktm = -1;
     ok = true;
   }
   for (int c = 0; c < 3; ++c) pwr[c] = pwr[c] * pmul[c];
@@ -2151,7 +2182,7 @@ __global__ void __launch_bounds__(64) photon_kernel(SceneD S, uint64_t seed, lon
   V po, pd;
   photon_ray(L, seed, i, po, pd);
   new_wray(w, po, pd);
-  double kt[5] = {1, 1, 1, 1, 1};
+  int32_t kt = -1;  // the ray's medium (Child.ktm)
   int gen = 0;
   Best b = closest<false, F>(S, w, k, ct);
   if (b.t == DMAX) { cnt[gid] = 0; return; }
@@ -2165,7 +2196,7 @@ __global__ void __launch_bounds__(64) photon_kernel(SceneD S, uint64_t seed, lon
       double cur[3] = {pwr[0], pwr[1], pwr[2]};
       if (caustic_ray(S, h, kt, gen, cur, c)) {
         for (int q = 0; q < 3; ++q) pwr[q] = cur[q];
-        for (int q = 0; q < 5; ++q) kt[q] = c.kt[q];
+        kt = c.ktm;
         rgen = c.gen;
         k.node = (uint32_t)rgen;
         new_wray(w, c.o, c.d);
@@ -2220,7 +2251,7 @@ __global__ void __launch_bounds__(64) photon_kernel(SceneD S, uint64_t seed, lon
         gen = gen + 1;
         k.node = bounce;
         new_wray(w, h.fwd, bd);
-        for (int q = 0; q < 5; ++q) kt[q] = 1;
+        kt = -1;
         b = closest<false, F>(S, w, k, ct);
         hit = b.t != DMAX;
         if (hit) h = make_hit<F>(S, b, w, k);
@@ -2232,7 +2263,7 @@ __global__ void __launch_bounds__(64) photon_kernel(SceneD S, uint64_t seed, lon
       double cur[3] = {pwr[0], pwr[1], pwr[2]};
       if (caustic_ray(S, h, kt, gen, cur, c)) {
         for (int q = 0; q < 3; ++q) pwr[q] = cur[q];
-        for (int q = 0; q < 5; ++q) kt[q] = c.kt[q];
+        kt = c.ktm;
         gen = c.gen;
         k.node = bounce;
         new_wray(w, c.o, c.d);

@@ -26,6 +26,7 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "nogather": ["RT_PROF_NOGATHER"],
     "knnheap": ["RT_KNN_HEAP"],
     "nophong": ["RT_PROF_NOPHONG"],
+    "notex": ["RT_PROF_NOTEX"],                # object textures -> plain diffuse
     "noshade": ["RT_PROF_NOSHADE"],            # camera rays traced, no hit record / shading
     "notrace": ["RT_PROF_NOTRACE"],            # camera rays generated, nothing traced
     "wprio": ["-Xarch_device", "-mllvm=--amdgpu-set-wave-priority"],  # compiler flags (results equal)
