@@ -52,50 +52,139 @@ static int upload(rt_scene* s, const std::vector<T>& v, const T** out) {
   return RT_OK;
 }
 
-// Conservative world-space bounding spheres of the top-level implicit primitives (spheres,
-// moving spheres, capped / hollow cylinders, rendered boxes): the object-space box of the
-// shape (a cylinder's y range widened by its 1e-7 acceptance slack), its 8 corners through
-// the CTM, the sphere around their box, inflated by 1e-6 relative + absolute. A ray that
-// misses it, or enters it beyond the current best hit / the shadow distance, cannot produce
-// a hit the reference would keep (closest / any-hit) -- see closest() / shadowed().
+// Conservative world-space bounds used to skip top-level entries a ray cannot hit
+// (closest() / shadowed(), trace_kernels.h top_culled):
+//  * implicit primitives (spheres, moving spheres, capped / hollow cylinders, rendered
+//    boxes): the object-space box of the shape (a cylinder's y range widened by its 1e-7
+//    acceptance slack), its 8 corners through the CTM;
+//  * BVHs / lists (TOP_ACCEL): every member's world geometry -- triangles enlarged by the
+//    reference's fat-edge acceptance (an inside test >= -1e-7 on unnormalised edge cross
+//    products accepts points up to 1e-7 / |edge| outside an edge, myPlanarObject.java:165-175),
+//    implicit members as above; lists holding quads, planes or instances get no bound.
+// Each becomes the sphere around the world box, inflated by 1e-6 relative + absolute. A ray
+// that misses it, or enters it beyond the current best hit / the shadow distance, cannot
+// produce a hit the reference would keep.
+static void box_union(double* mn, double* mx, const double* p) {
+  for (int c = 0; c < 3; ++c) { mn[c] = std::min(mn[c], p[c]); mx[c] = std::max(mx[c], p[c]); }
+}
+static void xform_pt(const double* g, const double* p, double* w) {
+  for (int r = 0; r < 3; ++r) w[r] = g[r * 4 + 0] * p[0] + g[r * 4 + 1] * p[1] + g[r * 4 + 2] * p[2] + g[r * 4 + 3];
+}
+// world box of an implicit primitive; false for other kinds
+static bool implicit_world_box(const HostScene& h, const PrimD& P, int xf, double* wmn, double* wmx) {
+  double mn[3], mx[3];
+  switch (P.type) {
+    case PT_SPHERE:
+    case PT_MSPHERE:
+      for (int c = 0; c < 3; ++c) {
+        const double r = std::fabs(P.a[3 + c]);
+        mn[c] = P.a[c] - r; mx[c] = P.a[c] + r;
+        if (P.type == PT_MSPHERE) { mn[c] = std::min(mn[c], P.a[6 + c] - r); mx[c] = std::max(mx[c], P.a[6 + c] + r); }
+      }
+      break;
+    case PT_CYL:
+    case PT_HCYL: {
+      const double rx = std::fabs(P.a[3]), rz = std::fabs(P.a[4]);
+      mn[0] = P.a[0] - rx; mx[0] = P.a[0] + rx;
+      mn[2] = P.a[2] - rz; mx[2] = P.a[2] + rz;
+      mn[1] = std::min(P.a[7], P.a[6]) - 1e-6; mx[1] = std::max(P.a[7], P.a[6]) + 1e-6;
+      break;
+    }
+    case PT_BOX:
+      for (int c = 0; c < 3; ++c) { mn[c] = P.a[c]; mx[c] = P.a[3 + c]; }
+      break;
+    default:
+      return false;
+  }
+  const double* g = h.xf[xf].g;
+  for (int k = 0; k < 8; ++k) {
+    const double p[3] = {(k & 1) ? mx[0] : mn[0], (k & 2) ? mx[1] : mn[1], (k & 4) ? mx[2] : mn[2]};
+    double w[3];
+    xform_pt(g, p, w);
+    box_union(wmn, wmx, w);
+  }
+  return true;
+}
+// world box of a triangle with its fat-edge acceptance region: in the triangle's plane each
+// edge line moves outward by 1e-7 / |edge| (plus slack); the enlarged triangle's corners are
+// the intersections of adjacent moved lines. False when an angle is too acute to bound.
+static bool tri_world_box(const HostScene& h, const TriD& T, double* wmn, double* wmx) {
+  const double* v[3] = {T.v[0], T.v[1], T.v[2]};
+  double e[3][3], len[3];
+  for (int i = 0; i < 3; ++i) {
+    const double* a = v[i];
+    const double* b = v[(i + 1) % 3];
+    for (int c = 0; c < 3; ++c) e[i][c] = b[c] - a[c];
+    len[i] = std::sqrt(e[i][0] * e[i][0] + e[i][1] * e[i][1] + e[i][2] * e[i][2]);
+    if (!(len[i] > 0) || !std::isfinite(len[i])) return false;
+  }
+  // corner i (at v[i], between edge i-1 and edge i, angle A): moving the two edge lines
+  // outward by da, db moves their intersection by sqrt(da^2 + db^2 + 2 da db cos A) / sin A
+  // <= (da + db) / sin A
+  double grow = 0;
+  for (int i = 0; i < 3; ++i) {
+    const int ia = (i + 2) % 3;
+    const double* ea = e[ia];  // into v[i]
+    const double* eb = e[i];   // out of v[i]
+    const double cosA = -(ea[0] * eb[0] + ea[1] * eb[1] + ea[2] * eb[2]) / (len[ia] * len[i]);
+    const double sinA = std::sqrt(std::max(0.0, 1 - cosA * cosA));
+    if (!(sinA > 1e-4)) return false;
+    const double da = 1e-7 / len[ia] * 1.01 + 1e-12, db = 1e-7 / len[i] * 1.01 + 1e-12;
+    grow = std::max(grow, (da + db) / sinA);
+  }
+  double mn[3], mx[3];
+  for (int c = 0; c < 3; ++c) {
+    mn[c] = std::min(v[0][c], std::min(v[1][c], v[2][c])) - grow;
+    mx[c] = std::max(v[0][c], std::max(v[1][c], v[2][c])) + grow;
+  }
+  const double* g = h.xf[T.xf].g;
+  for (int k = 0; k < 8; ++k) {
+    const double p[3] = {(k & 1) ? mx[0] : mn[0], (k & 2) ? mx[1] : mn[1], (k & 4) ? mx[2] : mn[2]};
+    double w[3];
+    xform_pt(g, p, w);
+    box_union(wmn, wmx, w);
+  }
+  return true;
+}
+// members of an accel: walk its node tree (rt_types.h child references)
+static bool accel_world_box(const HostScene& h, const AccelD& A, double* wmn, double* wmx) {
+  std::vector<int32_t> stack{A.root};
+  while (!stack.empty()) {
+    const int32_t r = stack.back();
+    stack.pop_back();
+    if (r >= 0) {
+      stack.push_back(h.node[r].left);
+      stack.push_back(h.node[r].right);
+      continue;
+    }
+    const int32_t c = ~r;
+    int32_t start, count;
+    const bool run = (c & LEAF_RUN_FLAG) != 0;
+    if (run) { start = (c >> 5) & LEAF_RUN_MAXSTART; count = c & 31; }
+    else { start = h.leaf[c].start; count = h.leaf[c].count; }
+    for (int i = 0; i < count; ++i) {
+      const int32_t m = run ? start + i : h.member[start + i];
+      if (m >= 0) {
+        if (!tri_world_box(h, h.tri[m], wmn, wmx)) return false;
+      } else {
+        const PrimD& P = h.prim[~m];
+        if (!implicit_world_box(h, P, P.xf, wmn, wmx)) return false;  // quads, planes, instances
+      }
+    }
+  }
+  return true;
+}
 static std::vector<double> top_bounds(const HostScene& h) {
   std::vector<double> b(4 * h.top.size(), -1.0);
   for (size_t i = 0; i < h.top.size(); ++i) {
     const TopD& t = h.top[i];
-    if (t.kind != TOP_PRIM) continue;
-    const PrimD& P = h.prim[t.idx];
-    double mn[3], mx[3];
-    switch (P.type) {
-      case PT_SPHERE:
-      case PT_MSPHERE:
-        for (int c = 0; c < 3; ++c) {
-          const double r = std::fabs(P.a[3 + c]);
-          mn[c] = P.a[c] - r; mx[c] = P.a[c] + r;
-          if (P.type == PT_MSPHERE) { mn[c] = std::min(mn[c], P.a[6 + c] - r); mx[c] = std::max(mx[c], P.a[6 + c] + r); }
-        }
-        break;
-      case PT_CYL:
-      case PT_HCYL: {
-        const double rx = std::fabs(P.a[3]), rz = std::fabs(P.a[4]);
-        mn[0] = P.a[0] - rx; mx[0] = P.a[0] + rx;
-        mn[2] = P.a[2] - rz; mx[2] = P.a[2] + rz;
-        mn[1] = std::min(P.a[7], P.a[6]) - 1e-6; mx[1] = std::max(P.a[7], P.a[6]) + 1e-6;
-        break;
-      }
-      case PT_BOX:
-        for (int c = 0; c < 3; ++c) { mn[c] = P.a[c]; mx[c] = P.a[3 + c]; }
-        break;
-      default:
-        continue;  // quads / planes / instances: never culled
-    }
-    const double* g = h.xf[t.xf].g;
     double wmn[3] = {1e300, 1e300, 1e300}, wmx[3] = {-1e300, -1e300, -1e300};
-    for (int k = 0; k < 8; ++k) {
-      const double p[3] = {(k & 1) ? mx[0] : mn[0], (k & 2) ? mx[1] : mn[1], (k & 4) ? mx[2] : mn[2]};
-      for (int r = 0; r < 3; ++r) {
-        const double w = g[r * 4 + 0] * p[0] + g[r * 4 + 1] * p[1] + g[r * 4 + 2] * p[2] + g[r * 4 + 3];
-        wmn[r] = std::min(wmn[r], w); wmx[r] = std::max(wmx[r], w);
-      }
+    if (t.kind == TOP_PRIM) {
+      if (!implicit_world_box(h, h.prim[t.idx], t.xf, wmn, wmx)) continue;  // quads / planes: never culled
+    } else if (t.kind == TOP_ACCEL) {
+      if (!accel_world_box(h, h.accel[t.idx], wmn, wmx)) continue;
+    } else {
+      continue;  // top-level triangles, instances
     }
     double c[3], hd2 = 0, cn = 0;
     for (int r = 0; r < 3; ++r) {
@@ -638,6 +727,14 @@ int rt_prof_pkstat_get(uint64_t* out) {  // profiling builds only: read and clea
   HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(dv::rt_pk_stat), 12 * sizeof(uint64_t)));
   const uint64_t z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dv::rt_pk_stat), z, sizeof(z)));
+  return RT_OK;
+}
+#endif
+#ifdef RT_PROF_REGIONS
+int rt_prof_regions_get(uint64_t* out) {  // profiling builds only: read and clear rt_prof_reg[16]
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(dv::rt_prof_reg), dv::R_N * sizeof(uint64_t)));
+  const uint64_t z[dv::R_N] = {};
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dv::rt_prof_reg), z, sizeof(z)));
   return RT_OK;
 }
 #endif

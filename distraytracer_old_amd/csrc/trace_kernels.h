@@ -143,6 +143,23 @@ __device__ unsigned long long rt_pk_stat[12];
 #else
 #define PKSTAT(step, m) do {} while (0)
 #endif
+#ifdef RT_PROF_REGIONS
+// profiling builds only (tools/regions.py): shader-clock cycles a wave spends in each region,
+// summed over waves (one atomic per region instance, by the first active lane). Regions nest:
+// the tool subtracts inner from outer regions.
+enum { R_CLOSEST, R_CLOSEST_ACCEL, R_SHADOW, R_SHADOW_ACCEL, R_HIT, R_TEX, R_LIGHT, R_SHADE, R_SAMPLE, R_KERNEL,
+       R_BG, R_PHOTON, R_N = 16 };
+__device__ unsigned long long rt_prof_reg[R_N];
+#define PROF_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(v, r)                                                                   \
+  do {                                                                                   \
+    const uint64_t pr_t_ = __builtin_amdgcn_s_memtime();                                 \
+    if (__lane_id() == (int)__builtin_ctzll(__ballot(1))) atomicAdd(&rt_prof_reg[r], (unsigned long long)(pr_t_ - (v))); \
+  } while (0)
+#else
+#define PROF_T0(v) do {} while (0)
+#define PROF_ADD(v, r) do {} while (0)
+#endif
 
 // a primitive test whose triangle record is loaded at a wave-uniform address (PK)
 template <bool CNT, uint32_t F, bool PK, class LIM = LimNone>
@@ -484,13 +501,14 @@ DEVI void inst_closest(const SceneD& S, int32_t ii, WRay& w, const Key& k, int t
   }
 }
 
-// Top-level culling of implicit primitives by their world bounding sphere (trace.hip
-// top_bounds, inflated 1e-6): true when the world ray (w.o, w.d, |w.d| = 1 after renorm)
-// misses the sphere or enters it beyond `lim` (the running best hit / the shadow distance),
-// so the primitive's own test could not produce a hit the reference keeps. Its sphere
-// contains every point the test can accept by a margin far above the test's rounding, so
-// the outcome is the reference's; the primitive's RNG draws are keyed, not a stream (Q23),
-// so skipping a test shifts nothing else.
+// Top-level culling by world bounding spheres (trace.hip top_bounds, inflated 1e-6): true
+// when the world ray (w.o, w.d, |w.d| = 1 after renorm) misses the sphere or enters it
+// beyond `lim` (the running best hit / the shadow distance), so the entry's own test could
+// not produce a hit the reference keeps. The sphere contains every point the test can
+// accept by a margin far above the test's rounding, so the outcome is the reference's; RNG
+// draws are keyed, not a stream (Q23), so skipping a test shifts nothing else. A BVH / list
+// entry re-normalises the ray in place in its leaves (myRay.java:93), so it is skipped only
+// for a ray that re-normalisation no longer changes (WRay.stable): callers check that.
 template <bool PK>
 DEVI bool top_culled(const SceneD& S, int i, const WRay& w, double lim) {
   const double* b = S.topBound + 4 * i;
@@ -501,8 +519,10 @@ DEVI bool top_culled(const SceneD& S, int i, const WRay& w, double lim) {
   const double tca = dot(oc, w.d), oc2 = dot(oc, oc);
   const double d2 = oc2 - tca * tca, R2 = R * R;
   if (d2 - R2 > 1e-9 * (oc2 + R2)) return true;  // misses the sphere
-  const double tn = tca - sqrt(fmax(R2 - d2, 0.0));
-  return tn > lim + 1e-9 * (fabs(lim) + sqrt(oc2) + R);  // enters it beyond lim
+  // enters it beyond lim: tca - sqrt(R2 - d2) > L, L = lim + 1e-9 (|lim| + |oc| + R), with
+  // |oc| <= (oc2 + 1) / 2 and the squares compared with slack (no square roots)
+  const double L = lim + 1e-9 * (fabs(lim) + 0.5 * (oc2 + 1) + R), a = tca - L, h2 = fmax(R2 - d2, 0.0);
+  return a > 0 && a * a > h2 * (1 + 1e-12) + 1e-12 * (oc2 + R2);
 }
 
 // findClosestRayHit (myScene.java:888-903): objList scan, TreeMap keeps the first of equal t
@@ -513,6 +533,7 @@ static constexpr bool PACKET = RT_PACKET != 0;  // render kernel: packet travers
 // PK: packet traversal of the BVHs (render kernel; the lanes of a wave are coherent)
 template <bool CNT, uint32_t F, bool PK = false>
 DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
+  PROF_T0(t_all);
   Best best = miss();
   for (int i = 0; i < S.ntop; ++i) {
     TopD tp = PK ? sload_top(S.top + i) : S.top[i];
@@ -523,7 +544,8 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       inst_closest<CNT, F>(S, tp.idx, w, k, i, best, local, ct);
       continue;
     }
-    if ((F & FT_PRIM) && tp.kind == TOP_PRIM && top_culled<PK>(S, i, w, best.t)) continue;
+    if ((((F & FT_PRIM) && tp.kind == TOP_PRIM) || (tp.kind == TOP_ACCEL && w.stable)) && top_culled<PK>(S, i, w, best.t))
+      continue;
     V o, d;
     if (PK) {  // wave-uniform records: scalar loads
       double inv[12];
@@ -540,8 +562,10 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       if (!box_hit(A.bmin, A.bmax, o, d, ri)) continue;
       w.moved = false;
       double local = DMAX;
+      PROF_T0(t_acc);
       if (PK) accel_closest_pk<CNT, F>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
       else accel_closest<CNT, F, false>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
+      PROF_ADD(t_acc, R_CLOSEST_ACCEL);
     } else {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
@@ -551,6 +575,7 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       }
     }
   }
+  PROF_ADD(t_all, R_CLOSEST);
   return best;
 }
 
@@ -691,7 +716,7 @@ DEVI bool inst_any(const SceneD& S, int32_t ii, const WRay& w, const Key& k, dou
 }
 // myScene.calcShadow (myScene.java:879-885)
 template <bool CNT, uint32_t F, bool PK = false>
-DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters& ct) {
+DEVI bool shadowed_(const SceneD& S, WRay& w, const Key& k, double dist, Counters& ct) {
   for (int i = 0; i < S.ntop; ++i) {
     TopD tp = PK ? sload_top(S.top + i) : S.top[i];
     if (CNT) ct.c[C_TOP]++;
@@ -700,7 +725,8 @@ DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters
       if (inst_any<CNT, F>(S, tp.idx, w, k, dist, ct)) return true;
       continue;
     }
-    if ((F & FT_PRIM) && tp.kind == TOP_PRIM && top_culled<PK>(S, i, w, dist)) continue;
+    if ((((F & FT_PRIM) && tp.kind == TOP_PRIM) || (tp.kind == TOP_ACCEL && w.stable)) && top_culled<PK>(S, i, w, dist))
+      continue;
     V o, d;
     if (PK) {  // wave-uniform records: scalar loads
       double inv[12];
@@ -713,9 +739,11 @@ DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters
     if (tp.kind == TOP_ACCEL) {
       if (CNT) ct.c[C_ROOT]++;
       w.moved = false;
-      if (PK ? accel_any_pk<CNT, F>(S, sload_accel(S.accel + tp.idx), o, d, w, k, dist, ct)
-             : accel_any<CNT, F, false>(S, S.accel[tp.idx], o, d, w, k, dist, ct))
-        return true;
+      PROF_T0(t_acc);
+      const bool blk = PK ? accel_any_pk<CNT, F>(S, sload_accel(S.accel + tp.idx), o, d, w, k, dist, ct)
+                          : accel_any<CNT, F, false>(S, S.accel[tp.idx], o, d, w, k, dist, ct);
+      PROF_ADD(t_acc, R_SHADOW_ACCEL);
+      if (blk) return true;
     } else {
       int32_t ref = tp.kind == TOP_TRI ? tp.idx : ~tp.idx;
       double t;
@@ -724,6 +752,13 @@ DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters
     }
   }
   return false;
+}
+template <bool CNT, uint32_t F, bool PK = false>
+DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters& ct) {
+  PROF_T0(t_all);
+  const bool r = shadowed_<CNT, F, PK>(S, w, k, dist, ct);
+  PROF_ADD(t_all, R_SHADOW);
+  return r;
 }
 
 // ---------------------------------------------------------------------------
@@ -1701,14 +1736,20 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
 #ifdef RT_PROF_NOGATHER  // profiling builds only: results differ
       V ir = mk(0, 0, 0);
 #else
+      PROF_T0(t_ph);
       V ir = irradiance<CNT>(S, h.fwd, ct);
+      PROF_ADD(t_ph, R_PHOTON);
 #endif
       if (m.isCausticPhtn) { r += ir.x; g += ir.y; b += ir.z; }
       else { r += m.diffuse[0] * ir.x; g += m.diffuse[1] * ir.y; b += m.diffuse[2] * ir.z; }
     }
   }
+  PROF_T0(t_tex);
   V tex = diff_color<CNT, F>(S, m, h, k, m.simple ? 1.0 : m.diffConst, ct);
+  PROF_ADD(t_tex, R_TEX);
+  PROF_T0(t_ls);
   V ls = light_sum<CNT, F>(S, m, h, tex, k, ct);
+  PROF_ADD(t_ls, R_LIGHT);
   r += ls.x; g += ls.y; b += ls.z;
   Fr.local = mk(r, g, b);
   branch = (in.gen < S.numRays - 2) && m.hasCaustic;
@@ -1800,17 +1841,23 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
       Best b = closest<CNT, F, PACKET>(S, w, k, ct);
 #endif
       if (b.t == DMAX) {
+        PROF_T0(t_bg);
         c = background<CNT, F>(S, w, ct);
+        PROF_ADD(t_bg, R_BG);
 #ifdef RT_PROF_NOSHADE
       } else if (true) {
         c = mk(b.t * 0.01, 0, 0);
 #endif
       } else {
+        PROF_T0(t_hit);
         HitRec h = make_hit<F>(S, b, w, k);
+        PROF_ADD(t_hit, R_HIT);
         bool branch;
         Child a;
         FrameOf<F>& Fr = fr[sp];
+        PROF_T0(t_sh);
         int nch = shade_node<CNT, F>(S, h, in, k, Fr, a, branch, ct);
+        PROF_ADD(t_sh, R_SHADE);
         if (nch > 0 && sp < MAX_FRAMES) {
           sp++;
           in = a;
@@ -1910,6 +1957,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   if (tile < 0) return;  // padding block of the XCD mapping (whole workgroup)
   if (P.order) tile = P.order[tile];
   const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();  // wave start (tcost / timeline)
+  PROF_T0(tk0);
   const int tx = tile % tilesX, ty = tile / tilesX;
   const int ci = tx * P.tw + pl % P.tw;  // column index within this render's columns
   const int col = (F & FT_PASS) ? ci * P.colStep : ci;
@@ -1999,7 +2047,9 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
         Key ks = k;
         ks.sample = (uint32_t)s;
         if (CNT) ct.c[C_CAMERA]++;
+        PROF_T0(t_smp);
         cc = trace_sample<CNT, F>(S, o, d, ks, ct);
+        PROF_ADD(t_smp, R_SAMPLE);
       }
     }
     if (G == 1) {
@@ -2044,6 +2094,9 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
 #endif
   }
   if (!CNT && P.tcost && lane == 0) P.tcost[tile] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tl0);
+#ifdef RT_PROF_REGIONS
+  if (!CNT) PROF_ADD(tk0, R_KERNEL);
+#endif
 #ifdef RT_PROF_TIMELINE
   if (!CNT && lane == 0 && rt_tl_buf) {
     unsigned long long* b = rt_tl_buf + 4 * (size_t)blockIdx.x;
