@@ -145,8 +145,8 @@ __device__ unsigned long long rt_pk_stat[12];
 #endif
 #ifdef RT_PROF_REGIONS
 // profiling builds only (tools/regions.py): shader-clock cycles a wave spends in each region,
-// summed over waves (one atomic per region instance, by the first active lane). Regions nest:
-// the tool subtracts inner from outer regions.
+// accumulated per wave in LDS by its first active lane (one wave per workgroup) and added to
+// the global sums once at the wave's end. Regions nest: the tool subtracts inner from outer.
 enum { R_CLOSEST, R_CLOSEST_ACCEL, R_SHADOW, R_SHADOW_ACCEL, R_HIT, R_TEX, R_LIGHT, R_SHADE, R_SAMPLE, R_KERNEL,
        R_BG, R_PHOTON, R_N = 16 };
 __device__ unsigned long long rt_prof_reg[R_N];
@@ -154,7 +154,7 @@ __device__ unsigned long long rt_prof_reg[R_N];
 #define PROF_ADD(v, r)                                                                   \
   do {                                                                                   \
     const uint64_t pr_t_ = __builtin_amdgcn_s_memtime();                                 \
-    if (__lane_id() == (int)__builtin_ctzll(__ballot(1))) atomicAdd(&rt_prof_reg[r], (unsigned long long)(pr_t_ - (v))); \
+    if (__lane_id() == (int)__builtin_ctzll(__ballot(1))) prof_acc(r, pr_t_ - (v));      \
   } while (0)
 #else
 #define PROF_T0(v) do {} while (0)
@@ -274,7 +274,12 @@ static constexpr int PKO_N = PKO_R + BVH_STACK * 8;
 static constexpr int PKO_C = PKO_N + BVH_STACK * 4;
 static constexpr int LDS_PK_BYTES = PKO_C + BVH_STACK * 4;
 static constexpr int LDS_MAX2 = LDS_STACK_BYTES > LDS_PK_BYTES ? LDS_STACK_BYTES : LDS_PK_BYTES;
-static constexpr int LDS_BYTES = LDS_MAX2 > 64 * 4 * 8 ? LDS_MAX2 : 64 * 4 * 8;
+static constexpr int LDS_BASE_BYTES = LDS_MAX2 > 64 * 4 * 8 ? LDS_MAX2 : 64 * 4 * 8;
+#ifdef RT_PROF_REGIONS
+static constexpr int LDS_BYTES = LDS_BASE_BYTES + R_N * 8;  // + the wave's region accumulators
+#else
+static constexpr int LDS_BYTES = LDS_BASE_BYTES;
+#endif
 typedef __attribute__((address_space(3))) double lds_f64;
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 DEVI lds_f64* ldsT() { return (lds_f64*)rt_lds; }
@@ -382,6 +387,10 @@ typedef __attribute__((address_space(3))) char lds_u8;
 DEVI lds_u8* pkB() { return (lds_u8*)rt_lds; }
 DEVI lds_f64* pkT() { return (lds_f64*)rt_lds; }
 DEVI lds_u64* pkM() { return (lds_u64*)(pkB() + PKO_M); }
+#ifdef RT_PROF_REGIONS
+DEVI lds_u64* profL() { return (lds_u64*)(pkB() + LDS_BASE_BYTES); }
+DEVI void prof_acc(int r, uint64_t dt) { profL()[r] += dt; }
+#endif
 DEVI lds_u64* pkR() { return (lds_u64*)(pkB() + PKO_R); }
 DEVI lds_i32* pkN() { return (lds_i32*)(pkB() + PKO_N); }
 DEVI lds_i32* pkC() { return (lds_i32*)(pkB() + PKO_C); }
@@ -720,6 +729,19 @@ DEVI bool shadowed_(const SceneD& S, WRay& w, const Key& k, double dist, Counter
   for (int i = 0; i < S.ntop; ++i) {
     TopD tp = PK ? sload_top(S.top + i) : S.top[i];
     if (CNT) ct.c[C_TOP]++;
+#if defined(RT_PROF_SH_NOQUAD) || defined(RT_PROF_SH_NOIMPL)  // profiling builds only: results differ
+    if (tp.kind == TOP_PRIM) {
+      const bool bounded = sload(S.topBound + 4 * i + 3) > 0;
+#ifdef RT_PROF_SH_NOQUAD
+      if (!bounded) continue;
+#else
+      if (bounded) continue;
+#endif
+    }
+#endif
+#ifdef RT_PROF_SH_NOACCEL
+    if (tp.kind == TOP_ACCEL) continue;
+#endif
     renorm(w);
     if ((F & FT_INST) && tp.kind == TOP_INST) {
       if (inst_any<CNT, F>(S, tp.idx, w, k, dist, ct)) return true;
@@ -753,8 +775,13 @@ DEVI bool shadowed_(const SceneD& S, WRay& w, const Key& k, double dist, Counter
   }
   return false;
 }
+#ifdef RT_SHADOW_NOINLINE  // experiment: the shadow scan as a real call
+#define SHADOW_FN __device__ __attribute__((noinline))
+#else
+#define SHADOW_FN DEVI
+#endif
 template <bool CNT, uint32_t F, bool PK = false>
-DEVI bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters& ct) {
+SHADOW_FN bool shadowed(const SceneD& S, WRay& w, const Key& k, double dist, Counters& ct) {
   PROF_T0(t_all);
   const bool r = shadowed_<CNT, F, PK>(S, w, k, dist, ct);
   PROF_ADD(t_all, R_SHADOW);
@@ -1958,6 +1985,9 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   if (P.order) tile = P.order[tile];
   const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();  // wave start (tcost / timeline)
   PROF_T0(tk0);
+#ifdef RT_PROF_REGIONS
+  if (lane < R_N) profL()[lane] = 0;
+#endif
   const int tx = tile % tilesX, ty = tile / tilesX;
   const int ci = tx * P.tw + pl % P.tw;  // column index within this render's columns
   const int col = (F & FT_PASS) ? ci * P.colStep : ci;
@@ -2095,7 +2125,10 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   }
   if (!CNT && P.tcost && lane == 0) P.tcost[tile] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tl0);
 #ifdef RT_PROF_REGIONS
-  if (!CNT) PROF_ADD(tk0, R_KERNEL);
+  if (!CNT) {
+    PROF_ADD(tk0, R_KERNEL);
+    if (lane < R_N) atomicAdd(&rt_prof_reg[lane], (unsigned long long)profL()[lane]);
+  }
 #endif
 #ifdef RT_PROF_TIMELINE
   if (!CNT && lane == 0 && rt_tl_buf) {

@@ -36,7 +36,7 @@ def main():
     j = s.index(".amdhsa_kernel " + m.group(1))
     body = s[m.end():j].split("\n")
     files = dict(re.findall(r'^\s*\.file\s+(\d+)\s+"[^"]*"\s+"([^"]+)"', s, re.M))
-    depth, c, deep, where, loc = 0, Counter(), Counter(), Counter(), "?"
+    depth, c, deep, where, loc, bydepth = 0, Counter(), Counter(), Counter(), "?", Counter()
     for l in body:
         t = l.strip()
         ml = re.match(r"\.loc\s+(\d+)\s+(\d+)", t)
@@ -48,16 +48,20 @@ def main():
         if t and not t.startswith((".", ";")) and l.startswith("\t"):
             op = t.split()[0]
             c[op] += 1
-            if op.startswith("scratch_") and depth >= 2:
-                deep["st" if "store" in op else "ld"] += 1
-                where[(depth, "st" if "store" in op else "ld", loc)] += 1
+            if op.startswith(("scratch_", "buffer_")):  # private memory: arrays and spills
+                c["_priv"] += 1
+                bydepth[min(depth, 6)] += 1
+                if depth >= 2:
+                    deep["st" if "store" in op else "ld"] += 1
+                    where[(depth, "st" if "store" in op else "ld", loc)] += 1
     desc = s[s.index(".amdhsa_kernel " + m.group(1)):]
     g = lambda k: int(re.search(r"\.%s\s+(\d+)" % k, desc).group(1))
+    priv = c.pop("_priv", 0)
     ins = sum(c.values())
-    scr = sum(v for k, v in c.items() if k.startswith("scratch_"))
+    scr = priv
     print(f"F={F} ins={ins} scratch={scr} deep_st={deep['st']} deep_ld={deep['ld']} "
           f"private={g('amdhsa_private_segment_fixed_size')} vgpr_next={g('amdhsa_next_free_vgpr')} "
-          f"sgpr_next={g('amdhsa_next_free_sgpr')}")
+          f"sgpr_next={g('amdhsa_next_free_sgpr')} by_depth={dict(sorted(bydepth.items()))}")
     if lines:  # -g changes scheduling slightly: counts are indicative
         for (dp, kind, lc), v in sorted(where.items(), key=lambda x: -x[1])[:40]:
             print(f"  depth {dp} {kind} {lc}: {v}")

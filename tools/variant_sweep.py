@@ -38,6 +38,10 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "ed16sh12": ["RT_KNN_EDGES=16", "RT_KNN_SHELL=12"],
     "tl": ["RT_PROF_TIMELINE"],               # workgroup timeline (tools/timeline.py)
     "pkstat": ["RT_PROF_PKSTAT"],             # packet lane utilisation (tools/pkstat.py)
+    "shnoquad": ["RT_PROF_SH_NOQUAD"],         # shadow scan without quads / planes
+    "shnoimpl": ["RT_PROF_SH_NOIMPL"],         # shadow scan without implicit primitives
+    "shnoaccel": ["RT_PROF_SH_NOACCEL"],       # shadow scan without BVHs / lists
+    "shinline": ["RT_SHADOW_NOINLINE"],        # shadow scan as a real call (results equal)
     "regions": ["RT_PROF_REGIONS"],           # wave time per region (tools/regions.py)
 }
 FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS", "g": "RT_MAX_G", "p": "RT_PACKET",
