@@ -16,11 +16,16 @@ inside the timed region. Work per step is one frame whatever N is
 + refraction, counted exactly by an instrumented run before timing) / max-over-
 ranks step time.
 
-roofline: algorithmic bytes of the render kernel per launch (record sizes x the
-instrumented counters, DESIGN.md "Algorithmic bytes") / its mean duration from
-HIP events on the launch stream; peak 8000 GB/s (MI355X HBM3E). traffic: HBM
-bytes from a committed rocprofv3 --pmc FETCH_SIZE run (x2, gfx950 half-count) if
-present in profiles/, else null.
+roofline: algorithmic bytes of the render kernel per launch /
+its mean duration from HIP events on the launch stream; peak 8000 GB/s (MI355X HBM3E).
+The bytes are SURVEY 8(d)'s record sizes x the record loads the instrumented kernel counts
+-- once per WAVE step for records a wave loads once for all its lanes (packet traversal
+of BVHs and the photon map, wave-uniform top-level entries, lights), per lane otherwise
+(texels). The per-lane 8(d) figure (every lane charged for every record it tests) is
+reported beside it. traffic: measured HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE)
+from the newest committed rocprofv3 --pmc summary of the workload in profiles/, else
+null; fp64: the kernel's fp64 FLOP rate (same PMC summary) against the measured fp64
+VALU peak (tools/fp64_peak.hip).
 
 cpu_baseline: the oracle (CPU restatement of the reference path, fp64) timed on
 host cores on a row subsample of the same frame (rank 0, N=1 only).
@@ -41,6 +46,7 @@ sys.path.insert(0, str(REPO))
 METRIC = "Mray/s + achieved HBM GB/s, bun69k.cli 1024² 16spp, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_COPY_PEAK_GBPS = 6300.0  # measured float4-copy peak (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 74.07  # measured: tools/fp64_peak.hip on MI355X (profiles/r02_fp64_peak.json)
 
 # Algorithmic bytes per counted event: SURVEY.md 8(d)'s per-ray formula, records at the
 # sizes it states and no cache credit:
@@ -57,17 +63,29 @@ RECORD_BYTES = {
 }
 
 
+# the same records counted per wave step where a wave loads a record once for all its lanes
+# (RT_ST_W_*); texels are per-lane loads
+WAVE_RECORD_BYTES = {"w_node": 64, "w_tri": 48, "w_quad": 64, "w_implicit": 32, "w_light": 16, "w_photon": 32,
+                     "texel": 16}
+
+
 def algorithmic_bytes(st: dict) -> int:
+    """SURVEY 8(d) per-lane figure: every lane charged for every record it tests."""
     return int(sum(st.get(k, 0) * b for k, b in RECORD_BYTES.items()))
+
+
+def wave_bytes(st: dict) -> int:
+    """8(d) record sizes x record loads as the kernel issues them (per wave step / per lane)."""
+    return int(sum(st.get(k, 0) * b for k, b in WAVE_RECORD_BYTES.items()))
 
 
 def traced_rays(st: dict) -> int:
     return int(st["camera"] + st["shadow"] + st["refl"] + st["refr"])
 
 
-def find_traffic(workload: str):
-    """Per-launch HBM bytes from the newest committed PMC summary for this workload
-    (profiles/rNN_*pmc*.json; BENCH_TRAFFIC_JSON names one explicitly)."""
+def find_pmc(workload: str):
+    """The newest committed PMC summary for this workload (profiles/rNN_*pmc*.json, written by
+    tools/pmc_table.py / tools/pmc_summary.py; BENCH_TRAFFIC_JSON names one explicitly)."""
     files = sorted(glob.glob(str(REPO / "profiles" / "*pmc*.json")))
     if os.environ.get("BENCH_TRAFFIC_JSON"):
         files = [os.environ["BENCH_TRAFFIC_JSON"]]
@@ -77,7 +95,7 @@ def find_traffic(workload: str):
         except Exception:
             continue
         if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
-            return float(d["hbm_bytes_per_launch"]), Path(f).name
+            return d, Path(f).name
     return None, None
 
 
@@ -194,12 +212,13 @@ def main():
 
     # exact per-frame counters (instrumented run, outside the timed region)
     _, _, st = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=rstep, row_band=band)
-    counts = torch.tensor([traced_rays(st), algorithmic_bytes(st), st["camera"]], dtype=torch.float64,
+    counts = torch.tensor([traced_rays(st), algorithmic_bytes(st), st["camera"], wave_bytes(st)], dtype=torch.float64,
                           device=coll_dev)
     if dist:
         dist.all_reduce(counts)
-    rays_frame, bytes_frame, cam_frame = [float(x) for x in counts.tolist()]
+    rays_frame, bytes_frame, cam_frame, wbytes_frame = [float(x) for x in counts.tolist()]
     my_bytes = float(algorithmic_bytes(st))
+    my_wbytes = float(wave_bytes(st))
 
     # setup (untimed, like the counting run): a layout's first two renders calibrate its tile
     # dispatch order (probe, then measured wave times; rt_render_device in include/distraytracer.h)
@@ -236,9 +255,21 @@ def main():
 
     if rank == 0:
         # rank-0 kernel: its own algorithmic bytes over its own mean kernel duration
-        achieved = my_bytes / (kern_ms / 1e3) / 1e9
+        achieved = my_wbytes / (kern_ms / 1e3) / 1e9
+        achieved_lane = my_bytes / (kern_ms / 1e3) / 1e9
         workload = f"{args.config} {cli} {W}x{H} {spp}spp"
-        traffic, tsrc = find_traffic(workload) if world == 1 else (None, None)
+        pmc, tsrc = find_pmc(workload) if world == 1 else (None, None)
+        traffic = traffic_rd = traffic_wr = None
+        fp64 = None
+        if pmc:
+            traffic_rd = float(pmc["hbm_bytes_per_launch"])
+            traffic_wr = pmc.get("hbm_write_bytes_per_launch")
+            traffic = traffic_rd + float(traffic_wr or 0)
+            if pmc.get("fp64_flop_per_launch"):
+                tf = float(pmc["fp64_flop_per_launch"]) / (kern_ms / 1e3) / 1e12
+                fp64 = {"tflops": tf, "peak_tflops_measured": FP64_PEAK_TFLOPS, "frac": tf / FP64_PEAK_TFLOPS,
+                        "flop_per_launch": float(pmc["fp64_flop_per_launch"]),
+                        "note": "fp64 VALU wave instructions x 64 lanes (inactive lanes included: an upper bound)"}
         out = {
             "metric": METRIC,
             "value": rays_frame / (ms_per_step / 1e3) / 1e6,
@@ -263,13 +294,21 @@ def main():
             "host_build_s": host_build_s,
             "scene_load_s": scene_load_s,
             "photon_prepass_s": photon_s,
-            "achieved_hbm_gbps": achieved,
+            "algorithmic_gbps": achieved,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
                          "frac_vs_measured_copy_peak": achieved / HBM_COPY_PEAK_GBPS,
-                         "traffic": traffic, "traffic_source": tsrc,
+                         "traffic": traffic, "traffic_read": traffic_rd, "traffic_write": traffic_wr,
+                         "traffic_frac": (traffic / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBPS) if traffic else None,
+                         "traffic_source": tsrc,
                          "kernel": "render_kernel", "kernel_ms": kern_ms,
-                         "bytes_per_launch": my_bytes, "bytes_per_ray": bytes_frame / max(1.0, rays_frame)},
+                         "bytes_per_launch": my_wbytes, "bytes_per_ray": wbytes_frame / max(1.0, rays_frame),
+                         "accounting": "8(d) record sizes x record loads per wave step (packet / wave-uniform "
+                                       "records) or per lane (texels)",
+                         "achieved_8d_per_lane": achieved_lane, "frac_8d_per_lane": achieved_lane / HBM_PEAK_GBPS,
+                         "bytes_per_launch_8d_per_lane": my_bytes,
+                         "bytes_per_ray_8d_per_lane": bytes_frame / max(1.0, rays_frame),
+                         "fp64": fp64},
         }
         if world > 1 and args.backend == "gloo":
             out["rehearsal"] = f"gloo backend, {world} ranks on {ndev} GPU(s): not a scaling measurement"

@@ -29,7 +29,9 @@ enum : uint32_t {
   SITE_DISK = 0x100, SITE_SHADOW_TIME = 0x200, SITE_PH_DIR = 0x1000, SITE_PH_BOUNCE = 0x1100, SITE_PH_TIME = 0x1200
 };
 enum { C_CAMERA = 0, C_SHADOW, C_REFL, C_REFR, C_BOX, C_TRI, C_QUAD, C_IMPLICIT, C_LIGHT, C_PHOTON, C_TEXEL,
-       C_NODE, C_LEAF, C_MEMBER, C_ROOT, C_TOP, C_N = 16 };
+       C_NODE, C_LEAF, C_MEMBER, C_ROOT, C_TOP,
+       // record loads per wave step (include/distraytracer.h RT_ST_W_*)
+       C_WNODE, C_WTRI, C_WQUAD, C_WIMPLICIT, C_WLIGHT, C_WPHOTON, C_N = 24 };
 
 struct V {
   double x, y, z;

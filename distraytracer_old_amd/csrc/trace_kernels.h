@@ -56,15 +56,27 @@ struct HitCtx {
   uint32_t wver;
 };
 
-template <bool CNT, uint32_t F, class LIM = LimNone>
+// Counting kernel: one count per wave step, by the step's first active lane -- for records
+// a wave loads once for all its lanes (the C_W* counters)
+#define WCNT(idx, n)                                                                      \
+  do {                                                                                    \
+    if (CNT && __lane_id() == (int)__builtin_ctzll(__ballot(1))) ct.c[idx] += (n);        \
+  } while (0)
+// WAVE: the record address is wave-uniform (counted once per wave step), else per lane
+template <bool CNT, uint32_t F, class LIM = LimNone, bool WAVE = false>
 DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, double& t, int& args, Counters& ct,
                    const LIM& lim = LIM()) {
   if (!(F & FT_PRIM) || ref >= 0) {
     if (CNT) ct.c[C_TRI]++;
+    if (WAVE) WCNT(C_WTRI, 1); else if (CNT) ct.c[C_WTRI]++;
     return tri_test(S.tri[ref], o, d, t, args, lim);
   }
   const PrimD& P = S.prim[~ref];
-  if (CNT) { if (P.type == PT_QUAD || P.type == PT_PLANE) ct.c[C_QUAD]++; else ct.c[C_IMPLICIT]++; }
+  if (CNT) {
+    const int c = (P.type == PT_QUAD || P.type == PT_PLANE) ? C_QUAD : C_IMPLICIT;
+    ct.c[c]++;
+    if (WAVE) WCNT(c + (C_WQUAD - C_QUAD), 1); else ct.c[c + (C_WQUAD - C_QUAD)]++;
+  }
   return prim_test(P, o, d, k, t, args);
 }
 template <uint32_t F>
@@ -168,11 +180,12 @@ DEVI bool test_ref_u(const SceneD& S, int32_t ref, V o, V d, const Key& k, doubl
   if constexpr (PK) {
     if (!(F & FT_PRIM) || ref >= 0) {
       if (CNT) ct.c[C_TRI]++;
+      WCNT(C_WTRI, 1);
       const TriG T = sload_tri(S.tri + ref);
       return tri_test(T, o, d, t, args, lim);
     }
   }
-  return test_ref<CNT, F>(S, ref, o, d, k, t, args, ct, lim);
+  return test_ref<CNT, F, LIM, PK>(S, ref, o, d, k, t, args, ct, lim);
 }
 template <uint32_t F, bool PK>
 DEVI int32_t ref_xf_u(const SceneD& S, int32_t ref) {
@@ -339,7 +352,7 @@ DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, RayInv ri,
     // descend: push N, go left while the left box is hit
     while (N >= 0) {
       const NodeD& nd = S.node[N];
-      if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }  // both child boxes are tested once per visit
+      if (CNT) { ct.c[C_NODE]++; ct.c[C_WNODE]++; ct.c[C_BOX] += 2; }  // both child boxes are tested once per visit
       st.setT(sp, local);
       st.setN(sp, N << 1);
       sp++;
@@ -430,6 +443,7 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
       const ChildBox cl = sload_child(S.node + N, 0);
       st.setFrame(sp, N << 1, act);
       PKSTAT(P_CB_STEP, act);
+      WCNT(C_WNODE, 1);  // the node's record: left half now, right half at the unwind
       bool hl = false;
       if (in_mask(act)) {
         if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }
@@ -633,7 +647,7 @@ DEVI bool accel_any(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const
   while (true) {
     if (N >= 0) {  // internal: push (right child pending), go left if its box is hit
       const NodeD& nd = S.node[N];
-      if (CNT) ct.c[C_NODE]++;
+      if (CNT) { ct.c[C_NODE]++; ct.c[C_WNODE]++; }
       st.setN(sp++, N);
       if (shadow_box<CNT>(nd.lmin, nd.lmax, ao, ad, ri, dist, ct)) { N = nd.left; continue; }
     } else if (N != INT32_MAX) {
@@ -677,6 +691,7 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
       const ChildBox cl = sload_child(S.node + N, 0);
       const ChildBox cr = sload_child(S.node + N, 1);
       PKSTAT(P_AB_STEP, act);
+      WCNT(C_WNODE, 1);
       bool hl = false, hr = false;
       if (in_mask(act)) {
         if (CNT) ct.c[C_NODE]++;
@@ -1207,7 +1222,7 @@ DEVI V irradiance_heap(const SceneD& S, V p, Counters& ct) {
   while (true) {
     // N: a node to open
     const NodeD& nd = S.pnode[N];
-    if (CNT) ct.c[C_PHOTON]++;
+    if (CNT) { ct.c[C_PHOTON]++; ct.c[C_WPHOTON]++; }
     const double dl = box_d2(nd.lmin, nd.lmax, pos), dr = box_d2(nd.rmin, nd.rmax, pos);
     const bool vl = dl < maxd2, vr = dr < maxd2;
     // the nearer child now, the other one pushed (re-checked against the radius when popped)
@@ -1231,7 +1246,7 @@ DEVI V irradiance_heap(const SceneD& S, V p, Counters& ct) {
       if (child >= 0) { N = child; break; }
       // leaf: scan its photons
       const int start = side ? pn.pad[2] : pn.pad[0], count = side ? pn.padR[0] : pn.pad[1];
-      if (CNT) ct.c[C_PHOTON] += count;
+      if (CNT) { ct.c[C_PHOTON] += count; ct.c[C_WPHOTON] += count; }
       for (int q = 0; q < count; ++q) {
         const double* ph = S.ppos + 3 * (size_t)(start + q);
         const double dx = pos[0] - ph[0], dy = pos[1] - ph[1], dz = pos[2] - ph[2];
@@ -1283,7 +1298,7 @@ DEVI void photon_scan(const SceneD& S, const double* pos, double R2, Counters& c
   int32_t N = S.photonRoot;
   while (true) {
     const NodeD& nd = S.pnode[N];
-    if (CNT) ct.c[C_PHOTON]++;
+    if (CNT) { ct.c[C_PHOTON]++; ct.c[C_WPHOTON]++; }
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
       const double* mn = side ? nd.rmin : nd.lmin;
@@ -1292,7 +1307,7 @@ DEVI void photon_scan(const SceneD& S, const double* pos, double R2, Counters& c
       const int32_t c = side ? nd.right : nd.left;
       if (c >= 0) { st.setN(sp++, c); continue; }
       const int start = side ? nd.pad[2] : nd.pad[0], count = side ? nd.padR[0] : nd.pad[1];
-      if (CNT) ct.c[C_PHOTON] += count;
+      if (CNT) { ct.c[C_PHOTON] += count; ct.c[C_WPHOTON] += count; }
       for (int q = 0; q < count; ++q) {
         const double* ph = S.ppos + 3 * (size_t)(start + q);
         const double dx = pos[0] - ph[0], dy = pos[1] - ph[1], dz = pos[2] - ph[2];
@@ -1325,6 +1340,7 @@ DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters
   uint64_t act = __ballot(1);
   while (true) {
     if (CNT && in_mask(act)) ct.c[C_PHOTON]++;
+    WCNT(C_WPHOTON, 1);
     const NodeD* nd = S.pnode + N;
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
@@ -1341,6 +1357,7 @@ DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters
       }
       const int start = sload(side ? &nd->pad[2] : &nd->pad[0]), count = sload(side ? &nd->padR[0] : &nd->pad[1]);
       if (CNT && in_mask(m)) ct.c[C_PHOTON] += count;
+      WCNT(C_WPHOTON, count);
       for (int q0 = 0; q0 < count; q0 += PH_BATCH) {  // PH_BATCH photons' positions per scalar-load batch
         double px[PH_BATCH], py[PH_BATCH], pz[PH_BATCH];
 #pragma unroll
@@ -1610,6 +1627,7 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     double t = sqrt((((sr.o.x - lo2.x) * (sr.o.x - lo2.x)) + ((sr.o.y - lo2.y) * (sr.o.y - lo2.y))) + ((sr.o.z - lo2.z) * (sr.o.z - lo2.z)));
     double ltMult = 1;
     if (CNT) ct.c[C_LIGHT]++;
+    WCNT(C_WLIGHT, 1);  // the light record: scalar loads, once per wave
     if ((F & FT_LIGHTX) && ltype == 1) {  // mySpotLight.intersectCheck / calcT_Mult (myLight.java:77-82,159-163)
       double angle = jf::acos(-1 * dot(sr.d, ld3(L.orient)));
       ltMult = (angle < L.innerRad) ? 1 : (angle > L.outerRad) ? 0 : (L.outerRad - angle) / L.radDiff;

@@ -16,7 +16,11 @@ from . import build as _build
 from .scenes import SCENE_DIR, prepare
 
 ST_NAMES = ["camera", "shadow", "refl", "refr", "box", "tri", "quad", "implicit", "light", "photon", "texel",
-            "node", "leaf", "member", "root", "top"]
+            "node", "leaf", "member", "root", "top",
+            # the same record loads counted per wave step where a wave loads a record once for all
+            # its lanes (RT_ST_W_*, include/distraytracer.h)
+            "w_node", "w_tri", "w_quad", "w_implicit", "w_light", "w_photon"]
+RT_ST_N = 24
 INFO_NAMES = ["objects", "lights", "bvh_internal", "bvh_leaves", "bvh_depth", "bvh_prims", "prims",
               "rays_per_pixel", "device_bytes", "triangles", "photons", "materials", "photon_mode",
               "photon_count"]
@@ -253,12 +257,12 @@ class Scene:
         _check(lib().rt_render_pass(self._h, ctypes.byref(p), step, int(bool(skip_origin)), rgb.ctypes.data,
                                     argb.ctypes.data), "rt_render_pass")
 
-    def render_count(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, row_band=1):
-        p = params(W, H, spp, seed, rows, row_step, 0, row_band)
+    def render_count(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, row_band=1, flags=0):
+        p = params(W, H, spp, seed, rows, row_step, flags, row_band)
         n = nrows_of(p)
         rgb = np.zeros((n, W, 3), dtype=np.float32)
         argb = np.zeros((n, W), dtype=np.int32)
-        st = np.zeros(16, dtype=np.uint64)
+        st = np.zeros(RT_ST_N, dtype=np.uint64)
         _check(lib().rt_render_count(self._h, ctypes.byref(p), rgb.ctypes.data, argb.ctypes.data, st.ctypes.data),
                "rt_render_count")
         return rgb, argb, dict(zip(ST_NAMES, st[: len(ST_NAMES)].tolist()))

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 enum rt_status {
   RT_OK = 0,
@@ -184,7 +184,10 @@ typedef struct rt_scene rt_scene;
 enum {
   RT_ST_CAMERA = 0, RT_ST_SHADOW, RT_ST_REFL, RT_ST_REFR, RT_ST_BOX, RT_ST_TRI, RT_ST_QUAD, RT_ST_IMPLICIT,
   RT_ST_LIGHT, RT_ST_PHOTON, RT_ST_TEXEL, RT_ST_NODE, RT_ST_LEAF, RT_ST_MEMBER, RT_ST_ROOT, RT_ST_TOP,
-  RT_ST_N = 16
+  /* the same record loads counted per WAVE step for records a wave loads once for all its
+     lanes (packet traversal, wave-uniform top-level entries and lights); per lane elsewhere */
+  RT_ST_W_NODE, RT_ST_W_TRI, RT_ST_W_QUAD, RT_ST_W_IMPLICIT, RT_ST_W_LIGHT, RT_ST_W_PHOTON,
+  RT_ST_N = 24
 };
 
 int rt_abi_version(void);

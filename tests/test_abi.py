@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(rt.EXPORTS)
-    assert L.rt_abi_version() == 3
+    assert L.rt_abi_version() == 4
 
 
 def test_no_gpu_fails_loudly():

@@ -17,5 +17,7 @@ timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_wri
 timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d $OUT/pmc_sq -o run -- python3 $B > $OUT/pmc_sq.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_BUSY_CYCLES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 --output-format csv -d $OUT/pmc_mem -o run -- python3 $B > $OUT/pmc_mem.log 2>&1
 rc=$?
+WL=$(python3 -c "import sys; sys.path.insert(0, '.'); from distraytracer_old_amd import scenes; c, W, H, s, _ = scenes.CONFIGS['$CFG']; print(f'$CFG {c} {W}x{H} {s}spp')")
+[ $rc -eq 0 ] && python3 tools/pmc_table.py $OUT --workload "$WL" --json $OUT/pmc.json > /dev/null
 echo "prof $CFG exit $rc" >> $OUT/status.txt
 exit $rc

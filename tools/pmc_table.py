@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-launch PMC means of the timed render kernel from tools/gpu_prof_cfg.sh output.
 
-  python tools/pmc_table.py gpurun_out/<tag>/<cfg> [--json out.json]
+  python tools/pmc_table.py gpurun_out/<tag>/<cfg> [--json out.json] [--workload "C3 c3_bun69k.cli 1024x1024 16spp"]
 
 Reads every pmc_*/run_counter_collection.csv under the directory, keeps the dispatches of
 the non-counting render kernel (render_kernel<false, F>), and prints each counter's mean
@@ -22,6 +22,7 @@ from collections import defaultdict
 def main():
     d = sys.argv[1]
     out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+    workload = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else None
     vals = defaultdict(list)
     kname = None
     for f in sorted(glob.glob(os.path.join(d, "pmc_*", "run_counter_collection.csv"))):
@@ -60,9 +61,16 @@ def main():
         der["fp64_tflops_upper"] = flops / (ms / 1e3) / 1e12
         if "SQ_INSTS_VALU" in mean:
             der["fp64_share_of_valu"] = sum(f64.values()) / mean["SQ_INSTS_VALU"]
-    print(json.dumps({"counters": mean, "derived": der}, indent=1))
+    out = {"workload": workload, "counters": mean, "derived": der,
+           # bench.py reads these (per launch of the timed render kernel)
+           "hbm_bytes_per_launch": der.get("hbm_read_bytes"), "hbm_write_bytes_per_launch": der.get("hbm_write_bytes"),
+           "fp64_flop_per_launch": der.get("fp64_flop_per_launch_upper"), "hbm_kernel": kname,
+           "method": "rocprofv3 --pmc, one pass per counter group; FETCH_SIZE x 1024 x 2 (gfx950 half-count), "
+                     "WRITE_SIZE x 1024; fp64 FLOP = 64 x (2 FMA + ADD + MUL) wave instructions (upper bound: "
+                     "inactive lanes counted)"}
+    print(json.dumps(out, indent=1))
     if out_json:
-        json.dump({"counters": mean, "derived": der}, open(out_json, "w"), indent=1)
+        json.dump(out, open(out_json, "w"), indent=1)
 
 
 if __name__ == "__main__":
