@@ -86,7 +86,7 @@ def traced_rays(st: dict) -> int:
 def find_pmc(workload: str):
     """The newest committed PMC summary for this workload (profiles/rNN_*pmc*.json, written by
     tools/pmc_table.py / tools/pmc_summary.py; BENCH_TRAFFIC_JSON names one explicitly)."""
-    files = sorted(glob.glob(str(REPO / "profiles" / "*pmc*.json")))
+    files = sorted(glob.glob(str(REPO / "profiles" / "*pmc*.json")))  # rNN<letter>_...: later runs sort later
     if os.environ.get("BENCH_TRAFFIC_JSON"):
         files = [os.environ["BENCH_TRAFFIC_JSON"]]
     for f in reversed(files):
