@@ -400,6 +400,21 @@ typedef __attribute__((address_space(3))) char lds_u8;
 DEVI lds_u8* pkB() { return (lds_u8*)rt_lds; }
 DEVI lds_f64* pkT() { return (lds_f64*)rt_lds; }
 DEVI lds_u64* pkM() { return (lds_u64*)(pkB() + PKO_M); }
+// Per-lane LDS spill slots for the shading of a hit (shade_node / light_sum, packet kernels):
+// while a hit is shaded, the closest-hit traversal's per-lane subtree-minimum levels (pkT)
+// and the sample-colour buffer are idle -- shadow rays and the photon gather use only the
+// wave-uniform frames -- so the values that must outlive every shadow-ray scan (normal, view
+// direction, texture colour, the light sums) wait there instead of in VGPRs, and the scan's
+// traversal keeps its ray in registers. A compiler barrier after the stores makes every later
+// read come from LDS.
+// slots: while light_sum runs -- the node's ambient (+ photon) colour, ltMult, texture colour,
+// normal, view direction, light sums; between two rays of a shading tree -- the next ray.
+enum { SL_BASE = 0, SL_LTM = 3, SL_TEX = 4, SL_NRM = 7, SL_DW = 10, SL_RGB = 13, SL_N = 16, SL_RAYO = 0, SL_RAYD = 3 };
+DEVI void stash(int q, double v) { pkT()[q * 64 + __lane_id()] = v; }
+DEVI double unstash(int q) { return pkT()[q * 64 + __lane_id()]; }
+DEVI void stash3(int q, V v) { stash(q, v.x); stash(q + 1, v.y); stash(q + 2, v.z); }
+DEVI V unstash3(int q) { return mk(unstash(q), unstash(q + 1), unstash(q + 2)); }
+DEVI void lds_barrier() { asm volatile("" ::: "memory"); }
 #ifdef RT_PROF_REGIONS
 DEVI lds_u64* profL() { return (lds_u64*)(pkB() + LDS_BASE_BYTES); }
 DEVI void prof_acc(int r, uint64_t dt) { profL()[r] += dt; }
@@ -553,6 +568,12 @@ DEVI bool top_culled(const SceneD& S, int i, const WRay& w, double lim) {
 #define RT_PACKET 1
 #endif
 static constexpr bool PACKET = RT_PACKET != 0;  // render kernel: packet traversal
+// shade_node keeps the hit's normal / view direction / texture colour in the LDS slots while
+// its shadow rays are traced (stash() above); RT_STASH_SHADE=0 keeps them in registers
+#ifndef RT_STASH_SHADE
+#define RT_STASH_SHADE 1
+#endif
+static constexpr bool STASH_SHADE = PACKET && RT_STASH_SHADE != 0 && PK_LDS >= SL_N;
 // PK: packet traversal of the BVHs (render kernel; the lanes of a wave are coherent)
 template <bool CNT, uint32_t F, bool PK = false>
 DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
@@ -1589,8 +1610,12 @@ DEVI V disk_pos(const LightD& L, const Key& k, uint32_t kk) {  // getRandomDiskP
 // calcShadowColor (myObjShader.java:98-153)
 // pow for shading terms: integer exponents 0..1024 by binary exponentiation (within ~20
 // ulps of pow for the phong exponents used; ocml's double pow is ~40x the instructions)
+// the general pow as a real call: inlined, its polynomial constants are hoisted to the kernel
+// entry (loop-invariant VGPRs), spilled, and cost every wave a scratch round trip although
+// integer exponents never reach it
+__device__ __attribute__((noinline)) double pow_call(double x, double e) { return pow(x, e); }
 DEVI double pow_shade(double x, double e) {
-  if (!(e >= 0 && e <= 1024 && e == floor(e))) return pow(x, e);
+  if (!(e >= 0 && e <= 1024 && e == floor(e))) return pow_call(x, e);
   int n = (int)e;
   double r = 1, b = x;
   while (n) {
@@ -1600,10 +1625,13 @@ DEVI double pow_shade(double x, double e) {
   }
   return r;
 }
-template <bool CNT, uint32_t F>
+// STASH (packet kernels): h.nrm, h.dw and tex are in the LDS slots (shade_node), the sums too
+template <bool CNT, uint32_t F, bool STASH>
 DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const Key& k, Counters& ct) {
   double r = 0, g = 0, b = 0;
+  if (STASH) stash3(SL_RGB, mk(0, 0, 0));
   for (int li = 0; li < S.nlight; ++li) {
+    if (STASH) lds_barrier();
     const LightD& L = S.light[li];
     // li is wave-uniform: the light record's hot fields are scalar loads
     const int32_t ltype = sload(&L.type);
@@ -1640,14 +1668,23 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
 #ifdef RT_PROF_NOSHADOW  // profiling builds only (tools/variant_sweep.py): results differ
     if (false)
 #endif
+    if (STASH && (F & FT_LIGHTX)) { stash(SL_LTM, ltMult); lds_barrier(); }
     if (shadowed<CNT, F, PACKET>(S, sr, sk, t, ct)) continue;
     renorm(sr);  // shadowRay.direction._normalize()
-    double ldp = dot(sr.d, h.nrm) * ltMult;
-    if (ldp > EPS) {
-      r += tex.x * lcol.x * ldp;
-      g += tex.y * lcol.y * ldp;
-      b += tex.z * lcol.z * ldp;
+    if (STASH) {
+      if (F & FT_LIGHTX) ltMult = unstash(SL_LTM);
+      const V rgb = unstash3(SL_RGB);
+      r = rgb.x; g = rgb.y; b = rgb.z;
     }
+    const V hn = STASH ? unstash3(SL_NRM) : h.nrm;
+    double ldp = dot(sr.d, hn) * ltMult;
+    if (ldp > EPS) {
+      const V tx = STASH ? unstash3(SL_TEX) : tex;
+      r += tx.x * lcol.x * ldp;
+      g += tx.y * lcol.y * ldp;
+      b += tx.z * lcol.z * ldp;
+    }
+    if (STASH) stash3(SL_RGB, mk(r, g, b));
 #ifdef RT_PROF_NOPHONG  // profiling builds only: results differ
     continue;
 #endif
@@ -1655,16 +1692,19 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     // the specular term only adds colour (no hit / shadow / branch decision depends on it):
     // it is evaluated to a few ulps instead of the reference's exact operation order --
     // H normalised with one reciprocal, integer phong exponents by squaring
-    const V hv = mk(sr.d.x - h.dw.x, sr.d.y - h.dw.y, sr.d.z - h.dw.z);
+    const V hdw = STASH ? unstash3(SL_DW) : h.dw;
+    const V hv = mk(sr.d.x - hdw.x, sr.d.y - hdw.y, sr.d.z - hdw.z);
     const double hm = mag(hv), hr = hm == 0 ? 1.0 : 1.0 / hm;
-    double hdp = (hv.x * hr * h.nrm.x + hv.y * hr * h.nrm.y + hv.z * hr * h.nrm.z) * ltMult;
+    double hdp = (hv.x * hr * hn.x + hv.y * hr * hn.y + hv.z * hr * hn.z) * ltMult;
     if (hdp > EPS) {
       double ph = pow_shade(hdp * hdp, m.phong);
       r += m.specular[0] * lcol.x * ph;
       g += m.specular[1] * lcol.y * ph;
       b += m.specular[2] * lcol.z * ph;
+      if (STASH) stash3(SL_RGB, mk(r, g, b));
     }
   }
+  if (STASH) { lds_barrier(); return unstash3(SL_RGB); }
   return mk(r, g, b);
 }
 
@@ -1793,7 +1833,19 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
   V tex = diff_color<CNT, F>(S, m, h, k, m.simple ? 1.0 : m.diffConst, ct);
   PROF_ADD(t_tex, R_TEX);
   PROF_T0(t_ls);
-  V ls = light_sum<CNT, F>(S, m, h, tex, k, ct);
+  V ls;
+  HitRec hs = h;  // the hit as the rest of the node sees it (STASH: normal / view direction from LDS)
+  if constexpr (STASH_SHADE) {
+    stash3(SL_BASE, mk(r, g, b)); stash3(SL_TEX, tex); stash3(SL_NRM, h.nrm); stash3(SL_DW, h.dw);
+    lds_barrier();
+    ls = light_sum<CNT, F, true>(S, m, h, tex, k, ct);
+    lds_barrier();
+    hs.nrm = unstash3(SL_NRM); hs.dw = unstash3(SL_DW);
+    const V base = unstash3(SL_BASE);
+    r = base.x; g = base.y; b = base.z;
+  } else {
+    ls = light_sum<CNT, F, false>(S, m, h, tex, k, ct);
+  }
   PROF_ADD(t_ls, R_LIGHT);
   r += ls.x; g += ls.y; b += ls.z;
   Fr.local = mk(r, g, b);
@@ -1803,6 +1855,7 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
 #endif
   if (!branch) return 0;
   a.o = h.fwd;
+  if (STASH_SHADE) stash3(SL_RAYO, a.o);  // the child ray goes to trace_sample through LDS
   a.gen = in.gen + 1;
   a.node = in.node * 2;
   if constexpr ((F & FT_TRANS) != 0) {
@@ -1811,7 +1864,7 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
     if (trans || strans) {  // calcTransClr :157-276 / calcSimpleTransClr :503-631
       double ik[2];
       kt_of(S, in.ktm, ik);
-      const TransOut T = trans_split(m, h, ik, strans);
+      const TransOut T = trans_split(m, hs, ik, strans);
       // children's medium: the material's {KTrans, perm, permClr}; the simple shader's
       // reflection child gets all 1s
       Fr.mat = h.mat;
@@ -1820,6 +1873,7 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
       Fr.wb = T.tr;
       if (T.doA) {
         a.d = T.refr;
+        if (STASH_SHADE) stash3(SL_RAYD, a.d);
         a.ktm = h.mat;
         if (CNT) ct.c[C_REFR]++;
         Fr.phase = 1;
@@ -1834,6 +1888,7 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
       }
       if (T.doB) {  // only the reflection child: spawn it as "B"
         a.d = T.refl;
+        if (STASH_SHADE) stash3(SL_RAYD, a.d);
         a.node = in.node * 2 + 1;
         a.ktm = strans ? -1 : h.mat;
         if (CNT) ct.c[C_REFL]++;
@@ -1844,10 +1899,11 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
     }
   }
   if (m.krefl > 0.0) {  // calcReflClr :278-294
-    V back = mk(h.dw.x * -1, h.dw.y * -1, h.dw.z * -1);
-    V rd = refl_dir(back, h.nrm);
-    if (dot(rd, h.nrm) >= 0) {
+    V back = mk(hs.dw.x * -1, hs.dw.y * -1, hs.dw.z * -1);
+    V rd = refl_dir(back, hs.nrm);
+    if (dot(rd, hs.nrm) >= 0) {
       a.d = rd;
+      if (STASH_SHADE) stash3(SL_RAYD, a.d);
       a.ktm = -1;
       Fr.phase = 1;
       Fr.mat = h.mat;
@@ -1873,9 +1929,12 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
   int sp = 0;
   Child in;
   in.o = org; in.d = dir; in.node = 1; in.gen = 0; in.ktm = -1;
+  // STASH_SHADE: the next ray of the tree waits in LDS (stash slots) across the loop's back edge
+  if (STASH_SHADE) { stash3(SL_RAYO, in.o); stash3(SL_RAYD, in.d); }
   while (true) {
     V c;
     {
+      if (STASH_SHADE) { lds_barrier(); in.o = unstash3(SL_RAYO); in.d = unstash3(SL_RAYD); }
       WRay w;
       w.o = in.o; w.d = nrmz(in.d); w.d0 = w.d; w.stable = false; w.moved = false; w.ver = 0;  // myRay ctor
       k.node = in.node;
@@ -1905,7 +1964,7 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
         PROF_ADD(t_sh, R_SHADE);
         if (nch > 0 && sp < MAX_FRAMES) {
           sp++;
-          in = a;
+          in = a;  // STASH_SHADE: its o / d are already in the LDS slots (shade_node)
           continue;
         }
         c = branch ? clampc(add(Fr.local, mk(0, 0, 0))) : clampc(Fr.local);  // no child: acc stayed 0
@@ -1936,6 +1995,7 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
             P.acc = acc;
             in.o = P.org; in.d = P.dB; in.gen = P.gen + 1; in.node = P.node * 2 + 1;
             in.ktm = (mode == FM_SIMPLE) ? -1 : P.mat;
+            if (STASH_SHADE) { stash3(SL_RAYO, in.o); stash3(SL_RAYD, in.d); }
             if (CNT) ct.c[C_REFL]++;
             spawned = true;
             break;
