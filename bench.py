@@ -210,14 +210,19 @@ def main():
     rr = multigpu.RankRenderer(scene, W, H, spp, seed, dist, stage_host=(args.backend == "gloo"))
     r0, r1, rstep, band = rr.rows
 
-    # exact per-frame counters (instrumented run, outside the timed region)
+    # exact per-frame counters (instrumented runs, outside the timed region): the kernel as it
+    # runs (top-level culling on: the record loads it issues) and the reference algorithm's work
+    # (RT_RENDER_NOCULL: every objList entry tested for every ray, SURVEY 8(d)'s per-ray bytes)
     _, _, st = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=rstep, row_band=band)
-    counts = torch.tensor([traced_rays(st), algorithmic_bytes(st), st["camera"], wave_bytes(st)], dtype=torch.float64,
-                          device=coll_dev)
+    _, _, sr = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=rstep, row_band=band,
+                                  flags=rt.RENDER_NOCULL)
+    counts = torch.tensor([traced_rays(st), algorithmic_bytes(sr), st["camera"], wave_bytes(st), algorithmic_bytes(st)],
+                          dtype=torch.float64, device=coll_dev)
     if dist:
         dist.all_reduce(counts)
-    rays_frame, bytes_frame, cam_frame, wbytes_frame = [float(x) for x in counts.tolist()]
-    my_bytes = float(algorithmic_bytes(st))
+    rays_frame, bytes_frame, cam_frame, wbytes_frame, xbytes_frame = [float(x) for x in counts.tolist()]
+    my_bytes = float(algorithmic_bytes(sr))
+    my_xbytes = float(algorithmic_bytes(st))
     my_wbytes = float(wave_bytes(st))
 
     # setup (untimed, like the counting run): a layout's first two renders calibrate its tile
@@ -257,6 +262,7 @@ def main():
         # rank-0 kernel: its own algorithmic bytes over its own mean kernel duration
         achieved = my_wbytes / (kern_ms / 1e3) / 1e9
         achieved_lane = my_bytes / (kern_ms / 1e3) / 1e9
+        achieved_lane_x = my_xbytes / (kern_ms / 1e3) / 1e9
         workload = f"{args.config} {cli} {W}x{H} {spp}spp"
         pmc, tsrc = find_pmc(workload) if world == 1 else (None, None)
         traffic = traffic_rd = traffic_wr = None
@@ -305,9 +311,13 @@ def main():
                          "bytes_per_launch": my_wbytes, "bytes_per_ray": wbytes_frame / max(1.0, rays_frame),
                          "accounting": "8(d) record sizes x record loads per wave step (packet / wave-uniform "
                                        "records) or per lane (texels)",
+                         # SURVEY 8(d) per lane, the reference algorithm's work (nothing culled)
                          "achieved_8d_per_lane": achieved_lane, "frac_8d_per_lane": achieved_lane / HBM_PEAK_GBPS,
                          "bytes_per_launch_8d_per_lane": my_bytes,
                          "bytes_per_ray_8d_per_lane": bytes_frame / max(1.0, rays_frame),
+                         # ... and the same per-lane accounting of the work the kernel does (culling on)
+                         "frac_8d_per_lane_executed": achieved_lane_x / HBM_PEAK_GBPS,
+                         "bytes_per_ray_8d_per_lane_executed": xbytes_frame / max(1.0, rays_frame),
                          "fp64": fp64},
         }
         if world > 1 and args.backend == "gloo":
