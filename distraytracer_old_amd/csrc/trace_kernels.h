@@ -2039,6 +2039,30 @@ DEVI int tile_of_block(int b, int ntiles) {
 #ifndef RT_RENDER_WAVES
 #define RT_RENDER_WAVES 4
 #endif
+// where a lane's pixel is: sample lane j of pixel pl of the wave's tile
+struct PixGeo {
+  int j, pl, ci, col, ri, row;
+  bool valid;
+};
+template <uint32_t F>
+DEVI PixGeo pix_geo(int lane, int tile, int tilesX, int ncols, const ParamsD& P) {
+  PixGeo g;
+  g.j = lane & (P.G - 1);
+  g.pl = lane / P.G;
+  const int tx = tile % tilesX, ty = tile / tilesX;
+  g.ci = tx * P.tw + g.pl % P.tw;  // column index within this render's columns
+  g.col = (F & FT_PASS) ? g.ci * P.colStep : g.ci;
+  g.ri = ty * P.th + g.pl / P.tw;  // row index within this render's rows
+  g.valid = g.ci < ncols && g.ri < P.nrows;
+  g.row = P.row0 + (g.ri / P.band) * P.rowStep * P.band + g.ri % P.band;
+  return g;
+}
+// the lane index as an opaque value: what is derived from it is recomputed where it is used
+// instead of being hoisted out of the sample loop and kept (spilled) across the shading tree
+DEVI int opaque_lane(int lane) {
+  asm volatile("" : "+v"(lane));
+  return lane;
+}
 #ifdef RT_PROF_TIMELINE  // profiling builds only (tools/timeline.py): per-workgroup start/end clock + HW ids
 __device__ unsigned long long* rt_tl_buf;
 #endif
@@ -2053,7 +2077,6 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   double* cbuf = rt_lds;  // 64 x 4 doubles (colour, traced), aliases the traversal stack
   const int lane = threadIdx.x;
   const int G = P.G;
-  const int j = lane & (G - 1), pl = lane / G;
   // columns 0, colStep, ... of a refine pass; the other kernels render every column (the
   // column-step arithmetic alone cost the C3 kernel 2.4 %)
   const int ncols = (F & FT_PASS) ? (P.W + P.colStep - 1) / P.colStep : P.W;
@@ -2066,25 +2089,18 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
 #ifdef RT_PROF_REGIONS
   if (lane < R_N) profL()[lane] = 0;
 #endif
-  const int tx = tile % tilesX, ty = tile / tilesX;
-  const int ci = tx * P.tw + pl % P.tw;  // column index within this render's columns
-  const int col = (F & FT_PASS) ? ci * P.colStep : ci;
-  const int ri = ty * P.th + pl / P.tw;  // row index within this render's rows
-  const bool valid = ci < ncols && ri < P.nrows;
   Counters ct;
   if (CNT)
     for (int i = 0; i < P_N; ++i) ct.c[i] = 0;
-  const int row = P.row0 + (ri / P.band) * P.rowStep * P.band + ri % P.band;
-  const double rayY = (-1 * (row - P.H / 2.0));
-  const double rayX = col - P.W / 2.0;
   Key k;
   k.seed = P.seed;
-  k.pixel = (uint64_t)row * (uint64_t)P.W + (uint64_t)col;
   k.tsite = SITE_TIME;
   const int n = P.spp;
   const bool dof = (F & FT_DOF) && S.dof && !((F & FT_CAMX) && P.cam != 0);
   V fpt = mk(0, 0, 0), lc = mk(0, 0, 0);
-  if (dof && valid) {  // shootMultiDpthOfFldRays (myScene.java:1386-1406)
+  if (dof && pix_geo<F>(lane, tile, tilesX, ncols, P).valid) {  // shootMultiDpthOfFldRays (myScene.java:1386-1406)
+    const PixGeo g = pix_geo<F>(lane, tile, tilesX, ncols, P);
+    const double rayY = (-1 * (g.row - P.H / 2.0)), rayX = g.col - P.W / 2.0;
     lc = nrmz(mk(rayX, rayY, P.viewZ));
     // ray(eye, lc) hits the focal plane z = -focal (myPlane, identity CTM): the ctor and
     // getTransformedRay both normalise, then (o,1),(d,0) go through the identity inverse
@@ -2099,6 +2115,12 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   // per-pixel sums; the 1-spp non-DOF path (no averaging) keeps its one colour here instead
   double rs = 0, gs = 0, bs = 0;
   for (int s0 = 0; s0 < n; s0 += G) {
+    const PixGeo g = pix_geo<F>(opaque_lane(lane), tile, tilesX, ncols, P);
+    const int j = g.j, pl = g.pl, col = g.col, row = g.row;
+    const bool valid = g.valid;
+    const double rayY = (-1 * (row - P.H / 2.0));
+    const double rayX = col - P.W / 2.0;
+    k.pixel = (uint64_t)row * (uint64_t)P.W + (uint64_t)col;
     const int s = s0 + j;
     V cc = mk(0, 0, 0);
     bool traced = false;  // a fisheye sample outside the image circle adds nothing (myScene.java:1571)
@@ -2179,9 +2201,10 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
       __syncthreads();
     }
   }
-  if (valid && j == 0) {
+  const PixGeo g = pix_geo<F>(opaque_lane(lane), tile, tilesX, ncols, P);
+  if (g.valid && g.j == 0) {
     V c = (n == 1 && !dof) ? mk(rs, gs, bs) : clampc(mk(rs / n, gs / n, bs / n));
-    const size_t o = (size_t)ri * ncols + ci;
+    const size_t o = (size_t)g.ri * ncols + g.ci;
     if (rgb) {
       rgb[3 * o + 0] = (float)c.x;
       rgb[3 * o + 1] = (float)c.y;
