@@ -785,6 +785,9 @@ DEVI bool shadowed_(const SceneD& S, WRay& w, const Key& k, double dist, Counter
     }
     if ((((F & FT_PRIM) && tp.kind == TOP_PRIM) || (tp.kind == TOP_ACCEL && w.stable)) && top_culled<PK>(S, i, w, dist))
       continue;
+#ifdef RT_PROF_SH_SCANONLY  // profiling builds only: the scan (re-normalisation, culling) without the tests
+    continue;
+#endif
     V o, d;
     if (PK) {  // wave-uniform records: scalar loads
       double inv[12];
@@ -1665,10 +1668,10 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     Key sk = k;
     sk.tsite = SITE_SHADOW_TIME + li;
     PKSTAT(P_SH_STEP, __ballot(1));
+    if (STASH && (F & FT_LIGHTX)) { stash(SL_LTM, ltMult); lds_barrier(); }
 #ifdef RT_PROF_NOSHADOW  // profiling builds only (tools/variant_sweep.py): results differ
     if (false)
 #endif
-    if (STASH && (F & FT_LIGHTX)) { stash(SL_LTM, ltMult); lds_barrier(); }
     if (shadowed<CNT, F, PACKET>(S, sr, sk, t, ct)) continue;
     renorm(sr);  // shadowRay.direction._normalize()
     if (STASH) {

@@ -42,6 +42,8 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "shnoimpl": ["RT_PROF_SH_NOIMPL"],         # shadow scan without implicit primitives
     "shnoaccel": ["RT_PROF_SH_NOACCEL"],       # shadow scan without BVHs / lists
     "shinline": ["RT_SHADOW_NOINLINE"],        # shadow scan as a real call (results equal)
+    "shscan": ["RT_PROF_SH_SCANONLY"],         # shadow rays: the top-level scan only, no tests
+    "shnoacc": ["RT_PROF_SH_NOACCEL"],         # shadow rays: no BVH / list entries
     "regions": ["RT_PROF_REGIONS"],           # wave time per region (tools/regions.py)
 }
 FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS", "g": "RT_MAX_G", "p": "RT_PACKET",
