@@ -527,10 +527,10 @@ static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, 
   if (flags & RT_RENDER_NOCULL) sd.topBound = s->noCullBound;
   if (count) {  // counting always runs the all-features kernel
     HIPCHK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long) * RT_ST_N, st));
-    hipLaunchKernelGGL((dv::render_kernel<true, dv::FT_ALL>), grid, block, dv::LDS_BYTES, st, sd, P, d_rgb, d_argb,
+    hipLaunchKernelGGL((dv::render_kernel<true, dv::FT_ALL>), grid, block, dv::LDS_RENDER_BYTES, st, sd, P, d_rgb, d_argb,
                        (unsigned long long*)s->counters);
   } else {
-    hipLaunchKernelGGL(pick_variant(s->hs, flags), grid, block, dv::LDS_BYTES, st, sd, P, d_rgb, d_argb,
+    hipLaunchKernelGGL(pick_variant(s->hs, flags), grid, block, dv::LDS_RENDER_BYTES, st, sd, P, d_rgb, d_argb,
                        (unsigned long long*)nullptr);
   }
   HIPCHK(hipGetLastError());

@@ -293,6 +293,11 @@ static constexpr int LDS_BYTES = LDS_BASE_BYTES + R_N * 8;  // + the wave's regi
 #else
 static constexpr int LDS_BYTES = LDS_BASE_BYTES;
 #endif
+// render kernel: + the per-pixel colour sums of a multi-round sample loop (G >= 2: at most 32
+// pixels per wave), kept in LDS across the shading trees instead of in VGPRs
+static constexpr int SUM_BYTES = 32 * 3 * 8;
+static constexpr int LDS_RENDER_BYTES = LDS_BYTES + SUM_BYTES;
+static_assert(16 * LDS_RENDER_BYTES <= 160 * 1024, "16 waves per CU");
 typedef __attribute__((address_space(3))) double lds_f64;
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 DEVI lds_f64* ldsT() { return (lds_f64*)rt_lds; }
@@ -2115,8 +2120,18 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
     double t = -(dot(fN, fo) + S.lensFocal) / pr;
     fpt = mk(fd.x * t + fo.x, fd.y * t + fo.y, fd.z * t + fo.z);
   }
-  // per-pixel sums; the 1-spp non-DOF path (no averaging) keeps its one colour here instead
+  // per-pixel sums. SUMS_LDS variants keep them in LDS across the shading trees -- G >= 2 in
+  // sums[] (sample order), G == 1 (spp = 1, one round) as the lane's colour in cbuf; the others
+  // in registers (rs / gs / bs; the 1-spp non-DOF path keeps its one colour there). Which is
+  // faster depends on the variant's register allocation (measured: C3's F = 0 gains, C4's
+  // transparent variant loses 6 %).
+  constexpr bool SUMS_LDS = (F & FT_TRANS) == 0;
   double rs = 0, gs = 0, bs = 0;
+  lds_f64* sums = (lds_f64*)((lds_u8*)rt_lds + LDS_BYTES);
+  if (SUMS_LDS && G > 1 && (lane & (G - 1)) == 0) {
+    const int p = lane / G;
+    sums[3 * p] = 0; sums[3 * p + 1] = 0; sums[3 * p + 2] = 0;
+  }
   for (int s0 = 0; s0 < n; s0 += G) {
     const PixGeo g = pix_geo<F>(opaque_lane(lane), tile, tilesX, ncols, P);
     const int j = g.j, pl = g.pl, col = g.col, row = g.row;
@@ -2185,9 +2200,16 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
         PROF_ADD(t_smp, R_SAMPLE);
       }
     }
-    if (G == 1) {
-      if (n == 1 && !dof) { rs = cc.x; gs = cc.y; bs = cc.z; }
-      else if (traced) { rs += cc.x; gs += cc.y; bs += cc.z; }
+    if (G == 1) {  // one sample per pixel (G = 1 only for spp = 1): one round
+      if constexpr (SUMS_LDS) {  // its colour waits in cbuf
+        cbuf[4 * lane + 0] = cc.x;
+        cbuf[4 * lane + 1] = cc.y;
+        cbuf[4 * lane + 2] = cc.z;
+        cbuf[4 * lane + 3] = traced ? 1.0 : 0.0;
+      } else {
+        if (n == 1 && !dof) { rs = cc.x; gs = cc.y; bs = cc.z; }
+        else if (traced) { rs += cc.x; gs += cc.y; bs += cc.z; }
+      }
     } else {
       cbuf[4 * lane + 0] = cc.x;
       cbuf[4 * lane + 1] = cc.y;
@@ -2196,15 +2218,25 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
       __syncthreads();
       if (j == 0) {
         const int m = (n - s0) < G ? (n - s0) : G;
+        double sr = rs, sg = gs, sb = bs;
+        if (SUMS_LDS) { sr = sums[3 * pl]; sg = sums[3 * pl + 1]; sb = sums[3 * pl + 2]; }
         for (int q = 0; q < m; ++q) {
           const double* b = cbuf + 4 * (pl * G + q);
-          if (b[3] != 0) { rs += b[0]; gs += b[1]; bs += b[2]; }
+          if (b[3] != 0) { sr += b[0]; sg += b[1]; sb += b[2]; }
         }
+        if (SUMS_LDS) { sums[3 * pl] = sr; sums[3 * pl + 1] = sg; sums[3 * pl + 2] = sb; }
+        else { rs = sr; gs = sg; bs = sb; }
       }
       __syncthreads();
     }
   }
   const PixGeo g = pix_geo<F>(opaque_lane(lane), tile, tilesX, ncols, P);
+  if (SUMS_LDS && G > 1 && g.j == 0) { rs = sums[3 * g.pl]; gs = sums[3 * g.pl + 1]; bs = sums[3 * g.pl + 2]; }
+  if (SUMS_LDS && G == 1) {
+    const double* b = cbuf + 4 * lane;
+    if (n == 1 && !dof) { rs = b[0]; gs = b[1]; bs = b[2]; }  // the colour as traced (no averaging)
+    else if (b[3] != 0) { rs = 0 + b[0]; gs = 0 + b[1]; bs = 0 + b[2]; }  // the sum of one sample
+  }
   if (g.valid && g.j == 0) {
     V c = (n == 1 && !dof) ? mk(rs, gs, bs) : clampc(mk(rs / n, gs / n, bs / n));
     const size_t o = (size_t)g.ri * ncols + g.ci;
