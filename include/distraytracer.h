@@ -254,7 +254,9 @@ int rt_refine_steps(const rt_scene* scene, int width, int height, int* steps, in
    reference skips it on every pass after the first). p's row fields are ignored. Pixel RNG keys are
    the full render's, so the passes 16, 8, ..., 1 end in rt_render's image. */
 int rt_render_pass(rt_scene* scene, const rt_render_params* p, int step, int skip_origin, float* rgb, int32_t* argb);
-/* Instrumented render (per-lane counters, RT_ST_*): same image, slower; stats: uint64[RT_ST_N]. */
+/* Instrumented render (counters RT_ST_*: per lane, and RT_ST_W_* per wave step): same image,
+   slower; stats: uint64[RT_ST_N] (24 since ABI 4). RT_RENDER_NOCULL in p->flags counts the
+   reference algorithm's work (every objList entry tested). */
 int rt_render_count(rt_scene* scene, const rt_render_params* p, float* rgb, int32_t* argb, uint64_t* stats);
 /* Kernel-only timing helper: average ms of the render kernel over `iters` launches (HIP events on the
    launch stream), inputs resident in HBM; at least 2 warmup launches (the schedule calibration). */
