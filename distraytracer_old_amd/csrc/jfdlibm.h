@@ -31,6 +31,22 @@
 
 namespace jf {
 
+// JK(c): a polynomial / reduction constant. In the kernels it is materialised where it is
+// used (two v_mov_b32 in a volatile asm): left as literals, LICM hoists all of them to the
+// kernel entry as loop-invariant VGPRs, which are then spilled and reloaded from scratch at
+// every use. Elsewhere (oracle, host) it is the literal. The value is the same either way.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <uint64_t B>
+__device__ __forceinline__ double jk_() {
+  uint32_t lo, hi;
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(lo), "=v"(hi) : "i"((uint32_t)B), "i"((uint32_t)(B >> 32)));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+#define JK(c) (::jf::jk_<__builtin_bit_cast(uint64_t, (double)(c))>())
+#else
+#define JK(c) (c)
+#endif
+
 JF_FN uint64_t bits(double x) { return __builtin_bit_cast(uint64_t, x); }
 JF_FN double from_bits(uint64_t b) { return __builtin_bit_cast(double, b); }
 JF_FN int32_t hiw(double x) { return (int32_t)(bits(x) >> 32); }
@@ -40,9 +56,9 @@ JF_FN double sqrt_(double x) { return __builtin_sqrt(x); }  // IEEE correctly ro
 
 // k_sin.c: sin(x + y) on [-pi/4, pi/4], y the tail of x; iy = 0 means y is 0
 JF_FN double k_sin(double x, double y, int iy) {
-  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  const double S1 = JK(-1.66666666666666324348e-01), S2 = JK(8.33333333332248946124e-03),
+               S3 = JK(-1.98412698298579493134e-04), S4 = JK(2.75573137070700676789e-06),
+               S5 = JK(-2.50507602534068634195e-08), S6 = JK(1.58969099521155010221e-10);
   const int32_t ix = hiw(x) & 0x7fffffff;
   if (ix < 0x3e400000) return x;  // |x| < 2^-27
   const double z = x * x, v = z * x;
@@ -53,9 +69,9 @@ JF_FN double k_sin(double x, double y, int iy) {
 
 // k_cos.c: cos(x + y) on [-pi/4, pi/4]
 JF_FN double k_cos(double x, double y) {
-  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  const double C1 = JK(4.16666666666666019037e-02), C2 = JK(-1.38888888888741095749e-03),
+               C3 = JK(2.48015872894767294178e-05), C4 = JK(-2.75573143513906633035e-07),
+               C5 = JK(2.08757232129817482790e-09), C6 = JK(-1.13596475577881948265e-11);
   const int32_t ix = hiw(x) & 0x7fffffff;
   if (ix < 0x3e400000) return 1.0;  // |x| < 2^-27
   const double z = x * x;
@@ -68,10 +84,10 @@ JF_FN double k_cos(double x, double y) {
 
 // e_rem_pio2.c (medium range): x - n*pi/2 = y0 + y1, returns n
 JF_FN int rem_pio2(double x, double& y0, double& y1) {
-  const double invpio2 = 6.36619772367581382433e-01;
-  const double pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11;
-  const double pio2_2 = 6.07710050630396597660e-11, pio2_2t = 2.02226624879595063154e-21;
-  const double pio2_3 = 2.02226624871116645580e-21, pio2_3t = 8.47842766036889956997e-32;
+  const double invpio2 = JK(6.36619772367581382433e-01);
+  const double pio2_1 = JK(1.57079632673412561417e+00), pio2_1t = JK(6.07710050650619224932e-11);
+  const double pio2_2 = JK(6.07710050630396597660e-11), pio2_2t = JK(2.02226624879595063154e-21);
+  const double pio2_3 = JK(2.02226624871116645580e-21), pio2_3t = JK(8.47842766036889956997e-32);
   const int32_t hx = hiw(x), ix = hx & 0x7fffffff;
   if (ix <= 0x3fe921fb) { y0 = x; y1 = 0; return 0; }  // |x| <= pi/4
   if (ix < 0x4002d97c) {  // |x| < 3pi/4: n = +-1
@@ -143,20 +159,20 @@ JF_FN double cos(double x) {  // s_cos.c
 
 // rational approximation shared by e_asin.c / e_acos.c: R(z) = p(z) / q(z)
 JF_FN double asin_p(double z) {
-  const double pS0 = 1.66666666666666657415e-01, pS1 = -3.25565818622400915405e-01,
-               pS2 = 2.01212532134862925881e-01, pS3 = -4.00555345006794114027e-02,
-               pS4 = 7.91534994289814532176e-04, pS5 = 3.47933107596021167570e-05;
+  const double pS0 = JK(1.66666666666666657415e-01), pS1 = JK(-3.25565818622400915405e-01),
+               pS2 = JK(2.01212532134862925881e-01), pS3 = JK(-4.00555345006794114027e-02),
+               pS4 = JK(7.91534994289814532176e-04), pS5 = JK(3.47933107596021167570e-05);
   return z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
 }
 JF_FN double asin_q(double z) {
-  const double qS1 = -2.40339491173441421878e+00, qS2 = 2.02094576023350569471e+00,
-               qS3 = -6.88283971605453293030e-01, qS4 = 7.70381505559019352791e-02;
+  const double qS1 = JK(-2.40339491173441421878e+00), qS2 = JK(2.02094576023350569471e+00),
+               qS3 = JK(-6.88283971605453293030e-01), qS4 = JK(7.70381505559019352791e-02);
   return 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
 }
 
 JF_FN double acos(double x) {  // e_acos.c
-  const double pi = 3.14159265358979311600e+00, pio2_hi = 1.57079632679489655800e+00,
-               pio2_lo = 6.12323399573676603587e-17;
+  const double pi = JK(3.14159265358979311600e+00), pio2_hi = JK(1.57079632679489655800e+00),
+               pio2_lo = JK(6.12323399573676603587e-17);
   const int32_t hx = hiw(x), ix = hx & 0x7fffffff;
   if (ix >= 0x3ff00000) {  // |x| >= 1
     if (((ix - 0x3ff00000) | (int32_t)(uint32_t)bits(x)) == 0) return hx > 0 ? 0.0 : pi + 2.0 * pio2_lo;
@@ -179,8 +195,8 @@ JF_FN double acos(double x) {  // e_acos.c
 }
 
 JF_FN double asin(double x) {  // e_asin.c
-  const double pio2_hi = 1.57079632679489655800e+00, pio2_lo = 6.12323399573676603587e-17,
-               pio4_hi = 7.85398163397448278999e-01;
+  const double pio2_hi = JK(1.57079632679489655800e+00), pio2_lo = JK(6.12323399573676603587e-17),
+               pio4_hi = JK(7.85398163397448278999e-01);
   const int32_t hx = hiw(x), ix = hx & 0x7fffffff;
   if (ix >= 0x3ff00000) {  // |x| >= 1
     if (((ix - 0x3ff00000) | (int32_t)(uint32_t)bits(x)) == 0) return x * pio2_hi + x * pio2_lo;
