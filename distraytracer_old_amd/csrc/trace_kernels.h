@@ -160,7 +160,7 @@ __device__ unsigned long long rt_pk_stat[12];
 // accumulated per wave in LDS by its first active lane (one wave per workgroup) and added to
 // the global sums once at the wave's end. Regions nest: the tool subtracts inner from outer.
 enum { R_CLOSEST, R_CLOSEST_ACCEL, R_SHADOW, R_SHADOW_ACCEL, R_HIT, R_TEX, R_LIGHT, R_SHADE, R_SAMPLE, R_KERNEL,
-       R_BG, R_PHOTON, R_N = 16 };
+       R_BG, R_PHOTON, R_KNN_COUNT, R_KNN_FINAL, R_KNN_NPASS, R_KNN_NCALL, R_N = 16 };
 __device__ unsigned long long rt_prof_reg[R_N];
 #define PROF_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(v, r)                                                                   \
@@ -168,9 +168,14 @@ __device__ unsigned long long rt_prof_reg[R_N];
     const uint64_t pr_t_ = __builtin_amdgcn_s_memtime();                                 \
     if (__lane_id() == (int)__builtin_ctzll(__ballot(1))) prof_acc(r, pr_t_ - (v));      \
   } while (0)
+#define PROF_CNT(r)                                                                    \
+  do {                                                                                   \
+    if (__lane_id() == (int)__builtin_ctzll(__ballot(1))) prof_acc(r, 1);                \
+  } while (0)
 #else
 #define PROF_T0(v) do {} while (0)
 #define PROF_ADD(v, r) do {} while (0)
+#define PROF_CNT(r) do {} while (0)
 #endif
 
 // a primitive test whose triangle record is loaded at a wave-uniform address (PK)
@@ -1320,7 +1325,7 @@ DEVI V irradiance_heap(const SceneD& S, V p, Counters& ct) {
 
 // Photon scan: f(d2, photon) for every photon with d2 < R2 (photon BVH, depth first,
 // children pruned by box distance^2 >= R2; see box_d2). Order is irrelevant to its users.
-template <bool CNT, class Fn>
+template <bool CNT, bool PWR, class Fn>
 DEVI void photon_scan(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f) {
   NStack st;  // the ray-traversal stack is idle during shading
   int sp = 0;
@@ -1341,7 +1346,10 @@ DEVI void photon_scan(const SceneD& S, const double* pos, double R2, Counters& c
         const double* ph = S.ppos + 3 * (size_t)(start + q);
         const double dx = pos[0] - ph[0], dy = pos[1] - ph[1], dz = pos[2] - ph[2];
         const double d2 = dx * dx + dy * dy + dz * dz;  // myKD_Tree.find_near's distance, same order
-        if (d2 < R2) f(d2, start + q);
+        if (d2 < R2) {
+          const double* pw = S.ppwr + 3 * (size_t)(start + q);
+          f(d2, start + q, PWR ? mk(pw[0], pw[1], pw[2]) : mk(0, 0, 0));
+        }
       }
     }
     if (sp == 0) break;
@@ -1360,7 +1368,9 @@ DEVI void photon_scan(const SceneD& S, const double* pos, double R2, Counters& c
 #define RT_PH_BATCH 1
 #endif
 static constexpr int PH_BATCH = RT_PH_BATCH;
-template <bool CNT, class Fn>
+// PWR: the photon's power goes to f too, scalar-loaded with its position (the photon is
+// wave-uniform) instead of a dependent per-lane load inside f.
+template <bool CNT, bool PWR, class Fn>
 DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f) {
   lds_i32* fN = pkN();  // the ray traversal's wave-uniform frames (idle during shading)
   lds_u64* fM = pkM();
@@ -1389,18 +1399,25 @@ DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters
       WCNT(C_WPHOTON, count);
       for (int q0 = 0; q0 < count; q0 += PH_BATCH) {  // PH_BATCH photons' positions per scalar-load batch
         double px[PH_BATCH], py[PH_BATCH], pz[PH_BATCH];
+        V pw[PH_BATCH];
 #pragma unroll
         for (int j = 0; j < PH_BATCH; ++j)
           if (q0 + j < count) {
             const double* ph = S.ppos + 3 * (size_t)(start + q0 + j);
             px[j] = sload(ph); py[j] = sload(ph + 1); pz[j] = sload(ph + 2);
+            if (PWR) {
+              const double* pp = S.ppwr + 3 * (size_t)(start + q0 + j);
+              pw[j] = mk(sload(pp), sload(pp + 1), sload(pp + 2));
+            } else {
+              pw[j] = mk(0, 0, 0);
+            }
           }
 #pragma unroll
         for (int j = 0; j < PH_BATCH; ++j)
           if (q0 + j < count && in_mask(m)) {
             const double dx = pos[0] - px[j], dy = pos[1] - py[j], dz = pos[2] - pz[j];
             const double d2 = dx * dx + dy * dy + dz * dz;  // as photon_scan
-            if (d2 < R2) f(d2, start + q0 + j);
+            if (d2 < R2) f(d2, start + q0 + j, pw[j]);
           }
       }
     }
@@ -1410,10 +1427,10 @@ DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters
     act = uni64(fM[sp]);
   }
 }
-template <bool CNT, class Fn>
+template <bool CNT, bool PWR = false, class Fn>
 DEVI void photon_scan_any(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f) {
-  if (PACKET) photon_scan_pk<CNT>(S, pos, R2, ct, f);
-  else photon_scan<CNT>(S, pos, R2, ct, f);
+  if (PACKET) photon_scan_pk<CNT, PWR>(S, pos, R2, ct, f);
+  else photon_scan<CNT, PWR>(S, pos, R2, ct, f);
 }
 
 // The k nearest photons by selection instead of a heap (no per-lane memory): the
@@ -1432,8 +1449,17 @@ DEVI void photon_scan_any(const SceneD& S, const double* pos, double R2, Counter
 #ifndef RT_KNN_EDGES
 #define RT_KNN_EDGES 16
 #endif
+#ifndef RT_KNN_LDS_HIST
+#define RT_KNN_LDS_HIST 1
+#endif
 static constexpr int KNN_SHELL = RT_KNN_SHELL;
 static constexpr int KNN_EDGES = RT_KNN_EDGES;  // counters per counting pass
+// counting passes through a per-lane LDS histogram (packet kernels: the traversal stack's
+// pkT levels are idle during shading) instead of KNN_EDGES register counters
+static constexpr bool KNN_LDS_HIST = PACKET && RT_KNN_LDS_HIST != 0;
+static_assert(!KNN_LDS_HIST || KNN_EDGES * 64 * 4 <= PK_LDS * 64 * 8, "histogram fits the pkT levels");
+static_assert(!KNN_LDS_HIST || KNN_SHELL * 64 * 12 <= PK_LDS * 64 * 8, "window list fits the pkT levels");
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 template <bool CNT>
 DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
 #ifdef RT_KNN_HEAP
@@ -1480,45 +1506,82 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
     }
   }
   // --- bracket the k-th d^2: window [lo, hi), `below` photons under lo
+  PROF_CNT(R_KNN_NCALL);
   double lo = 0, hi = R2dens;
   int below = 0;
   bool all = false;  // fewer than K photons within max_dist: the set is all of them
   for (int level = 0; level < 32; ++level) {
+    PROF_T0(t_kc);
     constexpr int NE = KNN_EDGES;
-    double e[NE];
     const double w = (hi - lo) * (1.0 / NE);
+    // c(k) = photons with d2 < e[k] (including the `below` ones); the pass yields c(NE - 1)
+    // and the first edge kb with c(kb) >= K (-1: none), c(kb - 1) (0 for kb = 0) and c(kb)
+    uint32_t total = 0, cPrev = 0, cAt = 0;
+    int kb = -1;
+    if constexpr (KNN_LDS_HIST) {
+      // A photon goes to bucket j = #{k : e[k] <= d2} of a per-lane histogram in LDS and c(k)
+      // is its prefix sum. j0 from the scaled distance is biased low and raised by the exact
+      // edge compares, so j is exact: ~20 VALU per photon instead of 2 NE.
+      lds_u32* hist = (lds_u32*)pkT() + __lane_id();
 #pragma unroll
-    for (int k = 0; k < NE - 1; ++k) e[k] = lo + (k + 1) * w;
-    e[NE - 1] = hi;
-    uint32_t c[NE];  // photons with d2 < e[k] (including the `below` ones)
+      for (int k = 0; k < NE; ++k) hist[k * 64] = 0;
+      const double inv = NE / (hi - lo);
+      // the scaled distance and the edges carry rounding errors of ~4 NE hi / (hi - lo) 2^-52
+      // buckets: the 2^-12 bias covers them unless the window is 2^30 times narrower than hi
+      const bool narrow = !((hi - lo) > hi * 0x1p-30);
+      if (!__ballot(narrow)) {  // j0 is j or j - 1: one compare settles it (no loop)
+        const double lob = lo + 0x1p-12 * w;  // the bias, as a shifted origin
+        photon_scan_any<CNT>(S, pos, hi, ct, [&](double d2, int, V) {
+          // j0 <= NE: d2 < hi; a j0 of NE (rounding) can only mean j = NE - 1, as the min keeps
+          const int j0 = (int)fmax((d2 - lob) * inv, 0.0);
+          const int j = min(j0 + ((d2 < lo + (j0 + 1) * w) ? 0 : 1), NE - 1);  // e[j0] as below
+          __hip_atomic_fetch_add(hist + j * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        });
+      } else {  // some lane's window is too narrow for the bias: walk the edges from 0
+        photon_scan_any<CNT>(S, pos, hi, ct, [&](double d2, int, V) {
+          int j = 0;
+          while (j < NE - 1 && !(d2 < lo + (j + 1) * w)) ++j;
+          __hip_atomic_fetch_add(hist + j * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        });
+      }
+      for (int k = 0; k < NE; ++k) {
+        const uint32_t run = total + hist[k * 64];
+        if (kb < 0 && (int)run >= K) { kb = k; cPrev = total; cAt = run; }
+        total = run;
+      }
+    } else {
+      double e[NE];
 #pragma unroll
-    for (int k = 0; k < NE; ++k) c[k] = 0;
-    photon_scan_any<CNT>(S, pos, hi, ct, [&](double d2, int) {
+      for (int k = 0; k < NE - 1; ++k) e[k] = lo + (k + 1) * w;
+      e[NE - 1] = hi;
+      uint32_t c[NE];
 #pragma unroll
-      for (int k = 0; k < NE; ++k) c[k] += (d2 < e[k]) ? 1u : 0u;
-    });
-    if ((int)c[NE - 1] < K) {  // only possible for the start window: widen it
+      for (int k = 0; k < NE; ++k) c[k] = 0;
+      photon_scan_any<CNT>(S, pos, hi, ct, [&](double d2, int, V) {
+#pragma unroll
+        for (int k = 0; k < NE; ++k) c[k] += (d2 < e[k]) ? 1u : 0u;
+      });
+      total = c[NE - 1];
+#pragma unroll
+      for (int k = 0; k < NE; ++k)  // selects, no dynamic register indexing
+        if (kb < 0 && (int)c[k] >= K) { kb = k; cAt = c[k]; cPrev = k ? c[k - 1] : 0; }
+    }
+    PROF_ADD(t_kc, R_KNN_COUNT);
+    PROF_CNT(R_KNN_NPASS);
+    if ((int)total < K) {  // only possible for the start window: widen it
       if (hi == R2max) { all = true; break; }
       hi = (hi < R2far) ? R2far : R2max;
       continue;
     }
-    // first edge b with >= K photons below it (selects, no dynamic register indexing)
-    double nlo = lo, nhi = hi;
-    int nbelow = below, cb = (int)c[NE - 1];
-    bool found = false;
-#pragma unroll
-    for (int k = 0; k < NE; ++k) {
-      if (!found && (int)c[k] >= K) {
-        found = true;
-        nhi = e[k];
-        cb = (int)c[k];
-        if (k) { nlo = e[k - 1]; nbelow = (int)c[k - 1]; }
-      }
-    }
+    // the window becomes [e[kb - 1], e[kb]) with e[k] = lo + (k + 1) w, e[NE - 1] = hi
+    const double nhi = (kb == NE - 1) ? hi : lo + (kb + 1) * w;
+    const double nlo = kb ? lo + kb * w : lo;
+    const int nbelow = kb ? (int)cPrev : below, cb = (int)cAt;
     lo = nlo; hi = nhi; below = nbelow;
     if (cb - below <= KNN_SHELL || !(lo < hi)) break;
   }
   // --- final pass: every photon below the window, and the nearest K - below window photons
+  PROF_T0(t_kf);
   double sd[KNN_SHELL];
   int32_t si[KNN_SHELL];
 #pragma unroll
@@ -1526,25 +1589,49 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
   V res = mk(0, 0, 0);
   double rSq = 0;
   int n = 0;
-  photon_scan_any<CNT>(S, pos, all ? R2max : hi, ct, [&](double d2, int i) {
-    if (all || d2 < lo) {
-      const double* w = S.ppwr + 3 * (size_t)i;
-      res.x += w[0]; res.y += w[1]; res.z += w[2];
-      if (d2 > rSq) rSq = d2;
-      n++;
-    } else {  // window photon: keep the KNN_SHELL nearest, sorted (scan order breaks ties)
-      double xd = d2;
-      int32_t xi = i;
+  // window photon: keep the KNN_SHELL nearest, sorted (scan order breaks ties)
+  auto shell_insert = [&](double xd, int32_t xi) {
 #pragma unroll
-      for (int k = 0; k < KNN_SHELL; ++k) {
-        if (xd < sd[k]) {
-          const double td = sd[k]; const int32_t ti = si[k];
-          sd[k] = xd; si[k] = xi;
-          xd = td; xi = ti;
-        }
+    for (int k = 0; k < KNN_SHELL; ++k) {
+      if (xd < sd[k]) {
+        const double td = sd[k]; const int32_t ti = si[k];
+        sd[k] = xd; si[k] = xi;
+        xd = td; xi = ti;
       }
     }
-  });
+  };
+  if constexpr (KNN_LDS_HIST) {
+    // window photons are appended to a per-lane list in LDS during the scan and sorted once
+    // after it by the same insertion, in the same (scan) order. The window holds <= KNN_SHELL
+    // photons unless the bracket ran out of levels, which only a window of equal distances
+    // does: the list then keeps the first KNN_SHELL, as the sorted shell would.
+    lds_f64* ld = pkT() + __lane_id();
+    lds_i32* li = (lds_i32*)(pkT() + KNN_SHELL * 64) + __lane_id();
+    int m = 0;
+    photon_scan_any<CNT, true>(S, pos, all ? R2max : hi, ct, [&](double d2, int i, V w) {
+      if (all || d2 < lo) {
+        res.x += w.x; res.y += w.y; res.z += w.z;
+        if (d2 > rSq) rSq = d2;
+        n++;
+      } else {
+        if (m < KNN_SHELL) { ld[m * 64] = d2; li[m * 64] = i; }
+        m++;
+      }
+    });
+#pragma unroll
+    for (int k = 0; k < KNN_SHELL; ++k)
+      if (k < m) shell_insert(ld[k * 64], li[k * 64]);
+  } else {
+    photon_scan_any<CNT, true>(S, pos, all ? R2max : hi, ct, [&](double d2, int i, V w) {
+      if (all || d2 < lo) {
+        res.x += w.x; res.y += w.y; res.z += w.z;
+        if (d2 > rSq) rSq = d2;
+        n++;
+      } else {
+        shell_insert(d2, i);
+      }
+    });
+  }
   if (!all) {
     const int need = K - below;
 #pragma unroll
@@ -1556,6 +1643,7 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
         n++;
       }
   }
+  PROF_ADD(t_kf, R_KNN_FINAL);
   if (n == 0) return mk(0, 0, 0);  // [null] -> 0 (Q20)
   const double area = PI_F * rSq;
   return mk(res.x / area, res.y / area, res.z / area);

@@ -17,7 +17,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from distraytracer_old_amd import rt, scenes  # noqa: E402
 
 R = ["closest", "closest_accel", "shadow", "shadow_accel", "hit", "tex", "light", "shade", "sample", "kernel",
-     "bg", "photon"]
+     "bg", "photon", "knn_count", "knn_final", "knn_npass", "knn_ncall"]
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C4"
 cli, W, H, spp, seed = scenes.CONFIGS[cfg]
 if len(sys.argv) > 2:
@@ -41,6 +41,8 @@ parts = {
     "hit record": c["hit"],
     "texture": c["tex"],
     "photon gather": c["photon"],
+    "  of it: kNN counting passes": c["knn_count"],
+    "  of it: kNN final pass": c["knn_final"],
     "lights: shading (excl. shadow rays)": c["light"] - c["shadow"],
     "shadow: top-level loop": c["shadow"] - c["shadow_accel"],
     "shadow: BVH traversal": c["shadow_accel"],
@@ -48,5 +50,6 @@ parts = {
     "background": c["bg"],
     "trace tree: rest (frames)": c["sample"] - c["closest"] - c["hit"] - c["shade"] - c["bg"],
 }
-print(json.dumps({"cfg": cfg, "W": W, "H": H, "spp": spp, "raw": c,
+knn = {"passes_per_call": c["knn_npass"] / max(1.0, c["knn_ncall"]), "calls": c["knn_ncall"]}
+print(json.dumps({"cfg": cfg, "W": W, "H": H, "spp": spp, "raw": c, "knn_wave": knn,
                   "share": {n: round(v / k, 4) for n, v in parts.items()}}, indent=1))
