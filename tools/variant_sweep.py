@@ -39,6 +39,9 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "hist0": ["RT_KNN_LDS_HIST=0"],            # kNN counting in registers (results equal)
     "h32b2": ["RT_KNN_EDGES=32", "RT_PH_BATCH=2"],
     "h32sh12": ["RT_KNN_EDGES=32", "RT_KNN_SHELL=12"],
+    "sh10": ["RT_KNN_SHELL=10"],               # window list in LDS: up to 10 photons
+    "h32": ["RT_KNN_EDGES=32"],
+    "h32sh10": ["RT_KNN_EDGES=32", "RT_KNN_SHELL=10"],
     "tl": ["RT_PROF_TIMELINE"],               # workgroup timeline (tools/timeline.py)
     "pkstat": ["RT_PROF_PKSTAT"],             # packet lane utilisation (tools/pkstat.py)
     "shnoquad": ["RT_PROF_SH_NOQUAD"],         # shadow scan without quads / planes
