@@ -1434,8 +1434,10 @@ DEVI void photon_scan_any(const SceneD& S, const double* pos, double R2, Counter
 }
 
 // The k nearest photons by selection instead of a heap (no per-lane memory): the
-// k-th smallest d^2 is bracketed by counting passes -- KNN_EDGES (16) cumulative counters
-// against equally spaced edges of the current window [lo, hi) -- until the window holding the k-th
+// k-th smallest d^2 is bracketed by counting passes -- a histogram of equally spaced
+// buckets of the current window [lo, hi): 64 u16 buckets in LDS (knn_hist_pass; KNN_EDGES
+// = 16 u32 buckets when one lane has more than 65535 photons below hi, or 16 register
+// counters in builds without the packet kernels) -- until the window holding the k-th
 // photon has <= KNN_SHELL photons; a last pass sums every photon below the window and
 // the nearest (k - below) window photons (kept sorted in registers). Same k-set and
 // largest d^2 as the heap; the powers are summed in scan order rather than the
@@ -1444,7 +1446,7 @@ DEVI void photon_scan_any(const SceneD& S, const double* pos, double R2, Counter
 // around p holding >= k photons; if fewer than k photons fall below it, the next try is
 // that node's far-corner distance (all its photons lie within it), then max_dist^2.
 #ifndef RT_KNN_SHELL
-#define RT_KNN_SHELL 8
+#define RT_KNN_SHELL 10
 #endif
 #ifndef RT_KNN_EDGES
 #define RT_KNN_EDGES 16
@@ -1457,9 +1459,75 @@ static constexpr int KNN_EDGES = RT_KNN_EDGES;  // counters per counting pass
 // counting passes through a per-lane LDS histogram (packet kernels: the traversal stack's
 // pkT levels are idle during shading) instead of KNN_EDGES register counters
 static constexpr bool KNN_LDS_HIST = PACKET && RT_KNN_LDS_HIST != 0;
-static_assert(!KNN_LDS_HIST || KNN_EDGES * 64 * 4 <= PK_LDS * 64 * 8, "histogram fits the pkT levels");
+// KNN_H16: the LDS histogram as 64 u16 buckets (KNN_HB) instead of KNN_EDGES u32 ones
+#ifndef RT_KNN_H16
+#define RT_KNN_H16 1
+#endif
+#ifndef RT_KNN_H16_MAX  // photons per pass the u16 buckets take (lowered only to test the fallback)
+#define RT_KNN_H16_MAX 65535
+#endif
+static_assert(RT_KNN_H16_MAX <= 65535, "u16 buckets");
+static constexpr bool KNN_H16 = KNN_LDS_HIST && RT_KNN_H16 != 0;
+static constexpr int KNN_HB = KNN_H16 ? 64 : KNN_EDGES;
 static_assert(!KNN_LDS_HIST || KNN_SHELL * 64 * 12 <= PK_LDS * 64 * 8, "window list fits the pkT levels");
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// One counting pass over [lo, hi) through a per-lane LDS histogram (packet kernels: the
+// traversal stack's pkT levels are idle during shading) of NB equally spaced buckets:
+// bucket j = #{k : e[k] <= d2} with e[k] = lo + (k + 1) w (k < NB - 1), e[NB - 1] = hi, and
+// the counts c(k) = photons with d2 < e[k] (including those under lo) are its prefix sums.
+// Yields c(NB - 1) (total) and the first edge kb with c(kb) >= K (-1: none), c(kb - 1) (0 for
+// kb = 0) and c(kb). P16: two u16 buckets per LDS word (NB = 64 in the same 8 KB as 16 u32
+// ones, so the first pass narrows 4x further); ovf reports more than 65535 photons below hi,
+// whose counts may have carried between the halves (the caller repeats the pass with u32).
+template <bool CNT, int NB, bool P16>
+DEVI void knn_hist_pass(const SceneD& S, const double* pos, double lo, double hi, int K, Counters& ct,
+                        uint32_t& total, int& kb, uint32_t& cPrev, uint32_t& cAt, bool& ovf) {
+  constexpr int NW = P16 ? NB / 2 : NB;  // LDS words per lane
+  static_assert(NW * 64 * 4 <= PK_LDS * 64 * 8, "histogram fits the pkT levels");
+  lds_u32* hist = (lds_u32*)pkT() + __lane_id();
+#pragma unroll
+  for (int q = 0; q < NW; ++q) hist[q * 64] = 0;
+  uint32_t tot = 0;
+  auto bump = [&](int j) {
+    if (P16) {
+      __hip_atomic_fetch_add(hist + (j >> 1) * 64, 1u << ((j & 1) * 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      tot++;
+    } else {
+      __hip_atomic_fetch_add(hist + j * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+  };
+  const double w = (hi - lo) * (1.0 / NB);
+  const double inv = NB / (hi - lo);
+  // j0 from the scaled distance is biased low and raised by one exact edge compare, so j is
+  // exact: the scaled distance and the edges carry rounding errors of ~4 NB hi / (hi - lo)
+  // 2^-52 buckets, which the 2^-12 bias covers unless the window is 2^30 times narrower than hi
+  const bool narrow = !((hi - lo) > hi * 0x1p-30);
+  if (!__ballot(narrow)) {  // j0 is j or j - 1: one compare settles it (no loop)
+    const double lob = lo + 0x1p-12 * w;  // the bias, as a shifted origin
+    photon_scan_any<CNT>(S, pos, hi, ct, [&](double d2, int, V) {
+      // j0 <= NB: d2 < hi; a j0 of NB (rounding) can only mean j = NB - 1, as the min keeps
+      const int j0 = (int)fmax((d2 - lob) * inv, 0.0);
+      bump(min(j0 + ((d2 < lo + (j0 + 1) * w) ? 0 : 1), NB - 1));  // e[j0] as below
+    });
+  } else {  // some lane's window is too narrow for the bias: walk the edges from 0
+    photon_scan_any<CNT>(S, pos, hi, ct, [&](double d2, int, V) {
+      int j = 0;
+      while (j < NB - 1 && !(d2 < lo + (j + 1) * w)) ++j;
+      bump(j);
+    });
+  }
+  ovf = P16 && tot > (uint32_t)RT_KNN_H16_MAX;
+  for (int q = 0; q < NW; ++q) {
+    const uint32_t v = hist[q * 64];
+#pragma unroll
+    for (int h = 0; h < (P16 ? 2 : 1); ++h) {
+      const uint32_t run = total + (P16 ? ((v >> (16 * h)) & 0xffffu) : v);
+      if (kb < 0 && (int)run >= K) { kb = P16 ? 2 * q + h : q; cPrev = total; cAt = run; }
+      total = run;
+    }
+  }
+}
+
 template <bool CNT>
 DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
 #ifdef RT_KNN_HEAP
@@ -1513,43 +1581,24 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
   for (int level = 0; level < 32; ++level) {
     PROF_T0(t_kc);
     constexpr int NE = KNN_EDGES;
-    const double w = (hi - lo) * (1.0 / NE);
     // c(k) = photons with d2 < e[k] (including the `below` ones); the pass yields c(NE - 1)
     // and the first edge kb with c(kb) >= K (-1: none), c(kb - 1) (0 for kb = 0) and c(kb)
     uint32_t total = 0, cPrev = 0, cAt = 0;
     int kb = -1;
+    int ne = NE;  // this lane's edges in this pass: e[k] = lo + (k + 1) w, w = (hi - lo) / ne
     if constexpr (KNN_LDS_HIST) {
-      // A photon goes to bucket j = #{k : e[k] <= d2} of a per-lane histogram in LDS and c(k)
-      // is its prefix sum. j0 from the scaled distance is biased low and raised by the exact
-      // edge compares, so j is exact: ~20 VALU per photon instead of 2 NE.
-      lds_u32* hist = (lds_u32*)pkT() + __lane_id();
-#pragma unroll
-      for (int k = 0; k < NE; ++k) hist[k * 64] = 0;
-      const double inv = NE / (hi - lo);
-      // the scaled distance and the edges carry rounding errors of ~4 NE hi / (hi - lo) 2^-52
-      // buckets: the 2^-12 bias covers them unless the window is 2^30 times narrower than hi
-      const bool narrow = !((hi - lo) > hi * 0x1p-30);
-      if (!__ballot(narrow)) {  // j0 is j or j - 1: one compare settles it (no loop)
-        const double lob = lo + 0x1p-12 * w;  // the bias, as a shifted origin
-        photon_scan_any<CNT>(S, pos, hi, ct, [&](double d2, int, V) {
-          // j0 <= NE: d2 < hi; a j0 of NE (rounding) can only mean j = NE - 1, as the min keeps
-          const int j0 = (int)fmax((d2 - lob) * inv, 0.0);
-          const int j = min(j0 + ((d2 < lo + (j0 + 1) * w) ? 0 : 1), NE - 1);  // e[j0] as below
-          __hip_atomic_fetch_add(hist + j * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        });
-      } else {  // some lane's window is too narrow for the bias: walk the edges from 0
-        photon_scan_any<CNT>(S, pos, hi, ct, [&](double d2, int, V) {
-          int j = 0;
-          while (j < NE - 1 && !(d2 < lo + (j + 1) * w)) ++j;
-          __hip_atomic_fetch_add(hist + j * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        });
-      }
-      for (int k = 0; k < NE; ++k) {
-        const uint32_t run = total + hist[k * 64];
-        if (kb < 0 && (int)run >= K) { kb = k; cPrev = total; cAt = run; }
-        total = run;
+      bool ovf = false;
+      knn_hist_pass<CNT, KNN_HB, KNN_H16>(S, pos, lo, hi, K, ct, total, kb, cPrev, cAt, ovf);
+      ne = KNN_HB;
+      if (KNN_H16 && __ballot(ovf)) {  // > 65535 photons below hi: this pass again with u32 buckets
+        if (ovf) {
+          total = cPrev = cAt = 0; kb = -1;
+          knn_hist_pass<CNT, NE, false>(S, pos, lo, hi, K, ct, total, kb, cPrev, cAt, ovf);
+          ne = NE;
+        }
       }
     } else {
+      const double w = (hi - lo) * (1.0 / NE);
       double e[NE];
 #pragma unroll
       for (int k = 0; k < NE - 1; ++k) e[k] = lo + (k + 1) * w;
@@ -1573,9 +1622,11 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
       hi = (hi < R2far) ? R2far : R2max;
       continue;
     }
-    // the window becomes [e[kb - 1], e[kb]) with e[k] = lo + (k + 1) w, e[NE - 1] = hi
-    const double nhi = (kb == NE - 1) ? hi : lo + (kb + 1) * w;
-    const double nlo = kb ? lo + kb * w : lo;
+    // the window becomes [e[kb - 1], e[kb]) with e[k] = lo + (k + 1) w, e[ne - 1] = hi (the
+    // pass's w: (hi - lo) / ne, an exact power-of-two scaling either way)
+    const double wp = (hi - lo) * (ne == NE ? 1.0 / NE : 1.0 / KNN_HB);
+    const double nhi = (kb == ne - 1) ? hi : lo + (kb + 1) * wp;
+    const double nlo = kb ? lo + kb * wp : lo;
     const int nbelow = kb ? (int)cPrev : below, cb = (int)cAt;
     lo = nlo; hi = nhi; below = nbelow;
     if (cb - below <= KNN_SHELL || !(lo < hi)) break;

@@ -42,6 +42,10 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "sh10": ["RT_KNN_SHELL=10"],               # window list in LDS: up to 10 photons
     "h32": ["RT_KNN_EDGES=32"],
     "h32sh10": ["RT_KNN_EDGES=32", "RT_KNN_SHELL=10"],
+    "h64": ["RT_KNN_H16=1"],                   # 64 u16 LDS buckets per counting pass
+    "h64s10": ["RT_KNN_H16=1", "RT_KNN_SHELL=10"],
+    "h64ovf": ["RT_KNN_H16=1", "RT_KNN_SHELL=10", "RT_KNN_H16_MAX=300"],  # the u32 fallback on most passes
+    "h64s10reg": ["RT_KNN_H16=1", "RT_KNN_SHELL=10", "RT_PROF_REGIONS"],
     "tl": ["RT_PROF_TIMELINE"],               # workgroup timeline (tools/timeline.py)
     "pkstat": ["RT_PROF_PKSTAT"],             # packet lane utilisation (tools/pkstat.py)
     "shnoquad": ["RT_PROF_SH_NOQUAD"],         # shadow scan without quads / planes
