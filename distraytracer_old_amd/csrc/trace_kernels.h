@@ -1368,15 +1368,29 @@ DEVI void photon_scan(const SceneD& S, const double* pos, double R2, Counters& c
 #define RT_PH_BATCH 1
 #endif
 static constexpr int PH_BATCH = RT_PH_BATCH;
-// PWR: the photon's power goes to f too, scalar-loaded with its position (the photon is
+#ifndef RT_PH_VLOAD
+#define RT_PH_VLOAD 1
+#endif
+static constexpr int PH_VLOAD = RT_PH_VLOAD;  // leaf photons: vector load + v_readlane (0: scalar loads)
+DEVI double rdlane(double v, int L) {  // lane L's v (wave-uniform result)
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, L);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), L);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// PWR: the photon's power goes to f too, loaded with its position (the photon is
 // wave-uniform) instead of a dependent per-lane load inside f.
+// Leaf photons (PH_VLOAD, default): the i-th lane running the scan loads the leaf's i-th
+// photon (one coalesced vector load per leaf) and the photons are read back in leaf order
+// with v_readlane; leaves with more photons than running lanes take the scalar loads.
 template <bool CNT, bool PWR, class Fn>
 DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f) {
   lds_i32* fN = pkN();  // the ray traversal's wave-uniform frames (idle during shading)
   lds_u64* fM = pkM();
   int sp = 0;
   int32_t N = S.photonRoot;
-  uint64_t act = __ballot(1);
+  const uint64_t act_all = __ballot(1);  // the lanes running this scan
+  uint64_t act = act_all;
   while (true) {
     if (CNT && in_mask(act)) ct.c[C_PHOTON]++;
     WCNT(C_WPHOTON, 1);
@@ -1397,6 +1411,42 @@ DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters
       const int start = sload(side ? &nd->pad[2] : &nd->pad[0]), count = sload(side ? &nd->padR[0] : &nd->pad[1]);
       if (CNT && in_mask(m)) ct.c[C_PHOTON] += count;
       WCNT(C_WPHOTON, count);
+      if (PH_VLOAD && count <= __popcll(act_all)) {
+        // the leaf's photons as ONE coalesced vector load (the i-th active lane loads photon i),
+        // read back photon by photon with v_readlane: one memory round trip per leaf instead of
+        // one scalar load batch per photon
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act_all >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act_all, 0u));
+        double qx = 0, qy = 0, qz = 0;
+        V qw = mk(0, 0, 0);
+        if (rank < count) {
+          const double* ph = S.ppos + 3 * (size_t)(start + rank);
+          qx = ph[0]; qy = ph[1]; qz = ph[2];
+          if (PWR) {
+            const double* pp = S.ppwr + 3 * (size_t)(start + rank);
+            qw = mk(pp[0], pp[1], pp[2]);
+          }
+        }
+        uint64_t rem = act_all;  // lane of rank q: the q-th set bit
+        for (int q0 = 0; q0 < count; q0 += PH_VLOAD) {  // PH_VLOAD independent distances per step
+          double d2[PH_VLOAD];
+          V pw[PH_VLOAD];
+#pragma unroll
+          for (int j = 0; j < PH_VLOAD; ++j) {
+            const int L = (int)__builtin_ctzll(rem | (1ull << 63));  // past the leaf: any lane
+            rem &= rem - 1;
+            const double px = rdlane(qx, L), py = rdlane(qy, L), pz = rdlane(qz, L);
+            pw[j] = PWR ? mk(rdlane(qw.x, L), rdlane(qw.y, L), rdlane(qw.z, L)) : mk(0, 0, 0);
+            const double dx = pos[0] - px, dy = pos[1] - py, dz = pos[2] - pz;
+            d2[j] = dx * dx + dy * dy + dz * dz;  // as photon_scan
+          }
+          if (in_mask(m)) {
+#pragma unroll
+            for (int j = 0; j < PH_VLOAD; ++j)
+              if (q0 + j < count && d2[j] < R2) f(d2[j], start + q0 + j, pw[j]);
+          }
+        }
+        continue;
+      }
       for (int q0 = 0; q0 < count; q0 += PH_BATCH) {  // PH_BATCH photons' positions per scalar-load batch
         double px[PH_BATCH], py[PH_BATCH], pz[PH_BATCH];
         V pw[PH_BATCH];
