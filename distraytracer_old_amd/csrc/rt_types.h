@@ -149,6 +149,7 @@ struct SceneD {
   const double* ppwr;   // [nphoton][3]
   int32_t ntop, nlight, nphoton, photonRoot;
   int32_t photonK;
+  int32_t knnU16Max;  // photons per kNN counting pass the u16 buckets take (trace_kernels.h knn_hist_pass)
   double photonMaxD2;
   double bg[3];
   int32_t bkgTex;

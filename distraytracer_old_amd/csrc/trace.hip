@@ -226,6 +226,8 @@ static int upload_scene(rt_scene* s) {
   d.nphoton = 0;
   d.photonRoot = 0;
   d.photonK = h.photonK;
+  d.knnU16Max = 65535;  // DISTRAYTRACER_KNN_U16_MAX lowers it: a test of the u32 fallback
+  if (const char* e = std::getenv("DISTRAYTRACER_KNN_U16_MAX")) d.knnU16Max = std::max(0, std::min(65535, std::atoi(e)));
   d.photonMaxD2 = h.photonMaxD2;
   for (int c = 0; c < 3; ++c) d.bg[c] = h.bg[c];
   d.bkgTex = h.bkgTex;

@@ -1513,10 +1513,6 @@ static constexpr bool KNN_LDS_HIST = PACKET && RT_KNN_LDS_HIST != 0;
 #ifndef RT_KNN_H16
 #define RT_KNN_H16 1
 #endif
-#ifndef RT_KNN_H16_MAX  // photons per pass the u16 buckets take (lowered only to test the fallback)
-#define RT_KNN_H16_MAX 65535
-#endif
-static_assert(RT_KNN_H16_MAX <= 65535, "u16 buckets");
 static constexpr bool KNN_H16 = KNN_LDS_HIST && RT_KNN_H16 != 0;
 static constexpr int KNN_HB = KNN_H16 ? 64 : KNN_EDGES;
 static_assert(!KNN_LDS_HIST || KNN_SHELL * 64 * 12 <= PK_LDS * 64 * 8, "window list fits the pkT levels");
@@ -1566,7 +1562,7 @@ DEVI void knn_hist_pass(const SceneD& S, const double* pos, double lo, double hi
       bump(j);
     });
   }
-  ovf = P16 && tot > (uint32_t)RT_KNN_H16_MAX;
+  ovf = P16 && tot > (uint32_t)S.knnU16Max;
   for (int q = 0; q < NW; ++q) {
     const uint32_t v = hist[q * 64];
 #pragma unroll

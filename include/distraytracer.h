@@ -213,7 +213,10 @@ int rt_png_name(const char* save_name, char* buf, int cap);
 int rt_scene_save_name(const rt_scene* scene, char* buf, int cap);
 void rt_scene_destroy(rt_scene* scene);
 
-/* photon-map pre-pass (myScene.initRender :1096-1099); idempotent per scene */
+/* photon-map pre-pass (myScene.initRender :1096-1099); idempotent per scene. The kNN gather of
+   the render reads DISTRAYTRACER_KNN_U16_MAX (0..65535, default 65535) at rt_scene_create /
+   rt_scene_load_cli: the photons per counting pass its 16-bit buckets take before a lane
+   repeats the pass with 32-bit ones -- a testing knob; the image does not depend on it. */
 int rt_photons_build(rt_scene* scene, uint64_t seed);
 /* The photon map built by rt_photons_build as the reference's photon_list (myScene.java:1000-1091,
    insertion order): *count = number of photons; copies min(n, count) positions / powers

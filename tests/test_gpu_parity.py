@@ -182,6 +182,24 @@ def test_c5_full_prepass_and_k200_gather_parity():
     assert_exact_decisions(compare(rg, ag, ro, ao))
 
 
+def test_knn_u16_bucket_fallback_renders_identically(monkeypatch):
+    """The kNN counting passes keep 64 u16 buckets per lane and repeat a pass with 16 u32
+    buckets for a lane with more photons below the window's top than the u16 halves hold.
+    DISTRAYTRACER_KNN_U16_MAX (read at scene creation) lowers that threshold to 300, so most
+    first passes of C5's k = 200 gather take the fallback: the image must not change."""
+    seed = 0x5EED0005
+    imgs = []
+    for lim in (None, "300"):
+        if lim:
+            monkeypatch.setenv("DISTRAYTRACER_KNN_U16_MAX", lim)
+        g = rt.Scene.load_cli("t11.cli", textures={})
+        g.build_photons(seed)
+        imgs.append(g.render(64, 64, spp=2, seed=seed))
+    (r0, a0), (r1, a1) = imgs
+    assert np.array_equal(a0, a1)
+    assert np.array_equal(r0.view(np.uint32), r1.view(np.uint32))
+
+
 @pytest.mark.parametrize("cli,W,spp", [("c3_bun69k.cli", 128, 2), ("t01.cli", 128, 1), ("p2_t05.cli", 96, 2),
                                        ("c2clear.cli", 96, 1), ("plnts3ColsBunnies.cli", 96, 1),
                                        ("t11.cli", 64, 1), ("p3_t11_sierp.cli", 64, 1)])

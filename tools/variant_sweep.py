@@ -44,7 +44,6 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "h32sh10": ["RT_KNN_EDGES=32", "RT_KNN_SHELL=10"],
     "h64": ["RT_KNN_H16=1"],                   # 64 u16 LDS buckets per counting pass
     "h64s10": ["RT_KNN_H16=1", "RT_KNN_SHELL=10"],
-    "h64ovf": ["RT_KNN_H16=1", "RT_KNN_SHELL=10", "RT_KNN_H16_MAX=300"],  # the u32 fallback on most passes
     "vl": ["RT_PH_VLOAD=1"],                   # leaf photons: vector load + v_readlane
     "vl2": ["RT_PH_VLOAD=2"],                  # ... two independent distances per step
     "vl4": ["RT_PH_VLOAD=4"],
