@@ -14,7 +14,11 @@ CSRC = PKG / "csrc"
 LIB_DIR = PKG / "lib"
 LIB_PATH = LIB_DIR / "libdistraytracer.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["trace.hip", "photon_build.hip", "cli_loader.cpp", "scene_build.cpp", "photon.cpp"]
+SOURCES = ["trace.hip", "render_minreg.hip", "photon_build.hip", "cli_loader.cpp", "scene_build.cpp", "photon.cpp"]
+# per-source compiler flags: render_minreg.hip holds C3's and C5's render variants, which run
+# faster with the register-minimising scheduler (C4's variant, in trace.hip, runs slower with it)
+SOURCE_FLAGS = {"render_minreg.hip": ["-Xarch_device", "-mllvm=--amdgpu-sched-strategy=iterative-minreg",
+                                      "-Xarch_device", "-mllvm=--amdgpu-use-amdgpu-trackers=1"]}
 HEADERS = ["rt_types.h", "rt_internal.h", "host_math.h", "trace_device.h", "trace_kernels.h", "qdiv.h", "jfdlibm.h"]
 # -ffp-contract=off: keep the reference's (Java) unfused double arithmetic so discrete
 # decisions (hits, shadows, TIR) match the oracle; no fast-math (IEEE Inf/NaN needed).
@@ -44,7 +48,7 @@ def build(force: bool = False, verbose: bool = False, defines: list[str] | None 
         lang = [] if src.endswith(".hip") else ["-x", "c++"]
         # defines starting with "-" are extra compiler flags (tuning experiments)
         dflags = [d if d.startswith("-") else "-D" + d for d in (defines or [])]
-        cmd = [HIPCC, *COMPILE_FLAGS, *dflags, *lang, "-c", str(CSRC / src), "-o", str(obj)]
+        cmd = [HIPCC, *COMPILE_FLAGS, *SOURCE_FLAGS.get(src, []), *dflags, *lang, "-c", str(CSRC / src), "-o", str(obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         logs.append(r.stderr)
         if r.returncode != 0:

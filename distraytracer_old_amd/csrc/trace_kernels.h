@@ -33,8 +33,8 @@ enum : uint32_t {
   FT_ALL = 1023
 };
 
-__constant__ int c_perm[256];
-__constant__ int c_grad3[12][3];
+static __constant__ int c_perm[256];  // one copy per translation unit (trace.hip uploads its own)
+static __constant__ int c_grad3[12][3];
 
 // ---------------------------------------------------------------------------
 // a hit candidate: the world direction at test time is identified by the ray's
@@ -2259,6 +2259,16 @@ DEVI int opaque_lane(int lane) {
 #ifdef RT_PROF_TIMELINE  // profiling builds only (tools/timeline.py): per-workgroup start/end clock + HW ids
 __device__ unsigned long long* rt_tl_buf;
 #endif
+// C3's and C5's render variants are instantiated in render_minreg.hip, compiled with the
+// register-minimising machine scheduler (C3 -1.2 %, C5 -1 %; C4's variant loses 6 % with it, so
+// it and the others stay in trace.hip). Profiling builds keep every variant in trace.hip (their
+// counters are module globals read through trace.hip's module).
+#if defined(RT_PROF_PKSTAT) || defined(RT_PROF_REGIONS) || defined(RT_PROF_TIMELINE) || defined(RT_NO_SPLIT_TU)
+#define RT_SPLIT_TU 0
+#else
+#define RT_SPLIT_TU 1
+#endif
+static constexpr uint32_t F_C5 = FT_PRIM | FT_TRANS | FT_PHOTON | FT_LIGHTX;
 template <bool CNT, uint32_t F>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_RENDER_WAVES)))
 render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict__ argb, unsigned long long* __restrict__ gcount) {
@@ -2462,6 +2472,11 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
 #endif
 }
 
+#if RT_SPLIT_TU && !defined(RT_MINREG_TU)
+extern template __global__ void render_kernel<false, 0u>(SceneD, ParamsD, float*, int32_t*, unsigned long long*);
+extern template __global__ void render_kernel<false, F_C5>(SceneD, ParamsD, float*, int32_t*, unsigned long long*);
+#endif
+#ifndef RT_MINREG_TU  // the other kernels: trace.hip only
 // Tile cost probe for the dispatch schedule: one lane per tile traces the tile's first
 // pixel's un-jittered camera ray (closest hit only) and reports the work it counted.
 // Only the ORDER in which tiles are dispatched depends on it, never a pixel.
@@ -2685,5 +2700,6 @@ __global__ void __launch_bounds__(64) photon_kernel(SceneD S, uint64_t seed, lon
   cnt[gid] = n;
 }
 
+#endif  // RT_MINREG_TU
 }  // namespace dv
 }  // namespace rt

@@ -32,6 +32,10 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "wprio": ["-Xarch_device", "-mllvm=--amdgpu-set-wave-priority"],  # compiler flags (results equal)
     "itsched": ["-Xarch_device", "-mllvm=--amdgpu-sched-strategy=gcn-iterative-max-occupancy-experimental"],
     "bias0": ["-Xarch_device", "-mllvm=--amdgpu-schedule-metric-bias=0"],
+    "trk": ["-Xarch_device", "-mllvm=--amdgpu-use-amdgpu-trackers=1"],
+    "minreg": ["-Xarch_device", "-mllvm=--amdgpu-sched-strategy=iterative-minreg"],
+    "trkminreg": ["-Xarch_device", "-mllvm=--amdgpu-use-amdgpu-trackers=1", "-Xarch_device",
+                  "-mllvm=--amdgpu-sched-strategy=iterative-minreg"],
     "ed8": [],
     "ed16": ["RT_KNN_EDGES=16"],
     "ed32": ["RT_KNN_EDGES=32"],
