@@ -46,8 +46,15 @@ def build(force: bool = False, verbose: bool = False, defines: list[str] | None 
     for src in SOURCES:  # .hip -> device+host; .cpp -> host-only C++ (no device pass)
         obj = target.parent / (tag + src + ".o")
         lang = [] if src.endswith(".hip") else ["-x", "c++"]
-        # defines starting with "-" are extra compiler flags (tuning experiments)
-        dflags = [d if d.startswith("-") else "-D" + d for d in (defines or [])]
+        # defines starting with "-" are extra compiler flags, "@<source>:<flag>" a flag for one
+        # source only (tuning experiments)
+        dflags = []
+        for d in defines or []:
+            if d.startswith("@"):
+                s, f = d[1:].split(":", 1)
+                dflags += [f] if s == src else []
+            else:
+                dflags.append(d if d.startswith("-") else "-D" + d)
         cmd = [HIPCC, *COMPILE_FLAGS, *SOURCE_FLAGS.get(src, []), *dflags, *lang, "-c", str(CSRC / src), "-o", str(obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         logs.append(r.stderr)

@@ -33,6 +33,10 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "itsched": ["-Xarch_device", "-mllvm=--amdgpu-sched-strategy=gcn-iterative-max-occupancy-experimental"],
     "bias0": ["-Xarch_device", "-mllvm=--amdgpu-schedule-metric-bias=0"],
     "trk": ["-Xarch_device", "-mllvm=--amdgpu-use-amdgpu-trackers=1"],
+    # scheduler of trace.hip only (C4's variant and the others; C3 / C5 are in render_minreg.hip)
+    "c4ilp": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=max-ilp"],
+    "c4mmc": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=max-memory-clause"],
+    "c4itilp": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-ilp"],
     "minreg": ["-Xarch_device", "-mllvm=--amdgpu-sched-strategy=iterative-minreg"],
     "trkminreg": ["-Xarch_device", "-mllvm=--amdgpu-use-amdgpu-trackers=1", "-Xarch_device",
                   "-mllvm=--amdgpu-sched-strategy=iterative-minreg"],
