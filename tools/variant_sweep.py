@@ -34,6 +34,8 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "bias0": ["-Xarch_device", "-mllvm=--amdgpu-schedule-metric-bias=0"],
     "trk": ["-Xarch_device", "-mllvm=--amdgpu-use-amdgpu-trackers=1"],
     # scheduler of trace.hip only (C4's variant and the others; C3 / C5 are in render_minreg.hip)
+    "mrnohrp": ["@render_minreg.hip:-Xarch_device", "@render_minreg.hip:-mllvm=--amdgpu-disable-unclustered-high-rp-reschedule=1"],
+    "mrbias0": ["@render_minreg.hip:-Xarch_device", "@render_minreg.hip:-mllvm=--amdgpu-schedule-metric-bias=0"],
     "c4ilp": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=max-ilp"],
     "c4mmc": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=max-memory-clause"],
     "c4itilp": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-ilp"],
