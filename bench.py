@@ -7,9 +7,10 @@ workload C3 = scenes/c3_bun69k.cli (data/p3_t09.cli without `wood`) with the
 
 One step = one full C3 frame: every rank renders its rows (rank r renders the
 8-row bands r, r+N, r+2N, ... -- interleaved for load balance) with the HIP kernel into a
-device buffer, then (N>1) the per-rank float-RGB tiles are gathered to rank 0
+device buffer, then (N>1) the per-rank ARGB tiles are gathered to rank 0
 over RCCL (`dist.gather`: one point-to-point send per rank over xGMI) and
-re-interleaved there; frame i's exchange overlaps frame i+1's render
+re-interleaved there (the ARGB ints the reference's rndrdImg.pixels holds); frame i's exchange
+overlaps frame i+1's render
 (`multigpu.FrameExchange`, double-buffered tiles) and the last one is drained
 inside the timed region. Work per step is one frame whatever N is
 (strong scaling). value = traced rays of the frame (camera + shadow + reflection
@@ -23,12 +24,14 @@ The bytes are SURVEY 8(d)'s record sizes x the record loads the instrumented ker
 of BVHs and the photon map, wave-uniform top-level entries, lights), per lane otherwise
 (texels). The per-lane 8(d) figure (every lane charged for every record it tests) is
 reported beside it. traffic: measured HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE)
-from the newest committed rocprofv3 --pmc summary of the workload in profiles/, else
-null; fp64: the kernel's fp64 FLOP rate (same PMC summary) against the measured fp64
+from the newest committed rocprofv3 --pmc summary of the workload in profiles/ when it is of
+this library build (rt_build_id) and its kernel time is within 5 % of this run's, else null
+(traffic_missing says why); fp64: the kernel's fp64 FLOP rate (same PMC summary) against the measured fp64
 VALU peak (tools/fp64_peak.hip).
 
 cpu_baseline: the oracle (CPU restatement of the reference path, fp64) timed on
-host cores on a row subsample of the same frame (rank 0, N=1 only).
+the box's CPU share (affinity / cgroup quota / OMP_NUM_THREADS; the host's CPU count and model
+are recorded beside it) on the same frame (rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -83,26 +86,70 @@ def traced_rays(st: dict) -> int:
     return int(st["camera"] + st["shadow"] + st["refl"] + st["refr"])
 
 
-def find_pmc(workload: str):
-    """The newest committed PMC summary for this workload (profiles/rNN_*pmc*.json, written by
-    tools/pmc_table.py / tools/pmc_summary.py; BENCH_TRAFFIC_JSON names one explicitly)."""
+def find_pmc(workload: str, build_id: str, kern_ms: float):
+    """The newest committed PMC summary (profiles/rNN_*pmc*.json, written by tools/pmc_table.py;
+    BENCH_TRAFFIC_JSON names one explicitly) that describes THIS kernel: same workload, same
+    library build id (rt_build_id) and a kernel time within 5 % of this run's. Returns (summary,
+    file name, why-not): a summary of another build or a stale time is not used."""
     files = sorted(glob.glob(str(REPO / "profiles" / "*pmc*.json")))  # rNN<letter>_...: later runs sort later
     if os.environ.get("BENCH_TRAFFIC_JSON"):
         files = [os.environ["BENCH_TRAFFIC_JSON"]]
+    why = "no PMC summary of this workload in profiles/"
     for f in reversed(files):
         try:
             d = json.loads(Path(f).read_text())
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
-            return d, Path(f).name
-    return None, None
+        if d.get("workload") != workload or not d.get("hbm_bytes_per_launch"):
+            continue
+        pms = (d.get("derived") or {}).get("kernel_ms")
+        if d.get("build_id") != build_id:
+            why = f"newest summary {Path(f).name} is of build {d.get('build_id')}, not {build_id}"
+        elif not pms or abs(pms - kern_ms) > 0.05 * kern_ms:
+            why = f"{Path(f).name}: its kernel time {pms} ms is not within 5 % of this run's {kern_ms:.4f} ms"
+        else:
+            return d, Path(f).name, None
+        break  # only the newest summary of the workload is a candidate
+    return None, None, why
 
 
-def cpu_baseline(cli, W, H, spp, seed, tex, row_step=1, threads=16):
+def cpu_share() -> dict:
+    """The host CPUs this process may use (the box's share: its affinity mask and cgroup quota --
+    os.cpu_count() reports the whole machine's CPUs, which a shared box does not give us),
+    plus what the host has (lscpu's model name, nproc)."""
+    n_host = os.cpu_count() or 1
+    try:
+        n_aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n_aff = n_host
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    share = n_aff if quota is None else max(1, min(n_aff, int(quota)))
+    # the pool's rule for a one-GPU box: worker pools sized to its 16-CPU share (OMP_NUM_THREADS)
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(share, cap) if cap > 0 else share
+    return {"threads": threads, "host_cpus": n_host, "affinity_cpus": n_aff, "cgroup_cpu_quota": quota,
+            "omp_num_threads": cap or None, "cpu_model": model}
+
+
+def cpu_baseline(cli, W, H, spp, seed, tex, row_step=1):
     from oracle.oracle import OracleScene
 
-    threads = min(threads, os.cpu_count() or 1)
+    share = cpu_share()
+    threads = share["threads"]
     o = OracleScene(REPO / "scenes", cli, tex)
     o.render(W, H, spp=spp, seed=seed, rows=(0, H), row_step=512, threads=threads)  # warm caches
     t0 = time.perf_counter()
@@ -121,24 +168,41 @@ def cpu_baseline(cli, W, H, spp, seed, tex, row_step=1, threads=16):
         "kind": "port",
         "sample": f"oracle (fp64 C++ restatement) on rows 0::{row_step} of the {W}x{H}x{spp} frame "
                   f"({rays} rays, {dt:.2f} s on {threads} threads)",
+        "host": share,
         "value_1thread": traced_rays(st1) / dt1 / 1e6,
         "sample_1thread": f"rows 1::16 ({traced_rays(st1)} rays, {dt1:.2f} s, 1 thread)",
     }
 
 
+def visible_gpus() -> int:
+    """GPUs this process may use, counted without initialising HIP (a process that has initialised
+    the GPU must not start the ranks): the *_VISIBLE_DEVICES lists, else the KFD topology's GPU
+    nodes (/sys/class/kfd: nodes with a non-zero gpu_id)."""
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip()])
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id"):
+        try:
+            n += int(Path(f).read_text().strip() or 0) != 0
+        except (OSError, ValueError):
+            pass
+    return n
+
+
 def launch_ranks(args) -> int:
     """`bench.py --gpus N` (N > 1) started directly: start N ranks as ONE child process tree
     (torch.distributed.run, one rank per GPU, 127.0.0.1 rendezvous) and return its exit code.
-    Nothing here touches the GPU (device_count does not initialise HIP on this image)."""
+    Nothing here touches the GPU (visible_gpus reads sysfs / the environment, not HIP)."""
     import socket
     import subprocess
 
-    import torch
-
-    have = torch.cuda.device_count()
-    if args.backend == "nccl" and have < args.gpus:
-        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {have}", file=sys.stderr)
-        return 2
+    if args.backend == "nccl":  # gloo rehearsals share devices: no count needed
+        have = visible_gpus()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {have}", file=sys.stderr)
+            return 2
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -207,7 +271,8 @@ def main():
         multigpu.build_photons_sharded(scene, seed, info["photon_count"], dist, device=coll_dev)
         torch.cuda.synchronize()
         photon_s = time.perf_counter() - t
-    rr = multigpu.RankRenderer(scene, W, H, spp, seed, dist, stage_host=(args.backend == "gloo"))
+    # the exchanged frame is the reference's output, ARGB ints (rndrdImg.pixels): 4 bytes a pixel
+    rr = multigpu.RankRenderer(scene, W, H, spp, seed, dist, stage_host=(args.backend == "gloo"), planes=("argb",))
     r0, r1, rstep, band = rr.rows
 
     # exact per-frame counters (instrumented runs, outside the timed region): the kernel as it
@@ -231,7 +296,7 @@ def main():
     # ... then ~0.2 s of untimed frames: the GPU's clocks ramp over the first few launches
     t_warm = time.perf_counter()
     while time.perf_counter() - t_warm < 0.2:
-        rr.render(rr.rgb)
+        rr.render()
         torch.cuda.synchronize()
     for _ in range(args.warmup):
         rr.step()
@@ -264,7 +329,8 @@ def main():
         achieved_lane = my_bytes / (kern_ms / 1e3) / 1e9
         achieved_lane_x = my_xbytes / (kern_ms / 1e3) / 1e9
         workload = f"{args.config} {cli} {W}x{H} {spp}spp"
-        pmc, tsrc = find_pmc(workload) if world == 1 else (None, None)
+        bid = rt.build_id()
+        pmc, tsrc, why = find_pmc(workload, bid, kern_ms) if world == 1 else (None, None, "N > 1")
         traffic = traffic_rd = traffic_wr = None
         fp64 = None
         if pmc:
@@ -288,13 +354,14 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
+            "build_id": bid,
             "data": ("synthetic: bun69k = deterministic subdivision of data/bun500.cli (69,451 tris); "
                      "scene data/p3_t09.cli without the wood line") if args.config == "C3" else
                     f"scene scenes/{cli} (SURVEY 8(d) {args.config}); synthetic inputs where the reference's are missing",
             "config": {"workload": workload, "width": W, "height": H, "spp": spp, "seed": seed,
                        "rays_per_frame": int(rays_frame), "camera_samples": int(cam_frame),
                        "parallelism": f"{multigpu.BAND}-row bands interleaved over {world} rank(s)" +
-                                      (f" + {args.backend} gather of float RGB tiles to rank 0" if world > 1 else "")},
+                                      (f" + {args.backend} gather of the ARGB tiles to rank 0" if world > 1 else "")},
             "camera_msamples_per_s": cam_frame / (ms_per_step / 1e3) / 1e6,
             "kernel_ms_max_over_ranks": kern_ms_max,
             "host_build_s": host_build_s,
@@ -306,7 +373,9 @@ def main():
                          "frac_vs_measured_copy_peak": achieved / HBM_COPY_PEAK_GBPS,
                          "traffic": traffic, "traffic_read": traffic_rd, "traffic_write": traffic_wr,
                          "traffic_frac": (traffic / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBPS) if traffic else None,
-                         "traffic_source": tsrc,
+                         "traffic_source": tsrc, "traffic_build_id": pmc.get("build_id") if pmc else None,
+                         "traffic_kernel_ms": (pmc.get("derived") or {}).get("kernel_ms") if pmc else None,
+                         "traffic_missing": why,
                          "kernel": "render_kernel", "kernel_ms": kern_ms,
                          "bytes_per_launch": my_wbytes, "bytes_per_ray": wbytes_frame / max(1.0, rays_frame),
                          "accounting": "8(d) record sizes x record loads per wave step (packet / wave-uniform "

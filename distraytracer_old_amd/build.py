@@ -2,9 +2,17 @@
 
 The shared library is the product: HIP kernels + host scene builder + C ABI
 (include/distraytracer.h). It is built in-tree so it travels to the GPU box.
+
+Provenance: the build id is a hash of every source and header compiled into the library, the
+public header, and the compiler flags (this file's settings). It is compiled in (rt_build_id())
+and written next to the library (lib/libdistraytracer.buildinfo.json); a library whose id
+differs from the tree's is rebuilt, so a shipped .so is used only when it was built from these
+sources with these flags. build() reports whether it compiled or reused the library.
 """
 from __future__ import annotations
 
+import hashlib
+import json
 import os
 import subprocess
 from pathlib import Path
@@ -13,6 +21,8 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIB_DIR = PKG / "lib"
 LIB_PATH = LIB_DIR / "libdistraytracer.so"
+INFO_PATH = LIB_DIR / "libdistraytracer.buildinfo.json"
+PUBLIC_HEADER = PKG.parent / "include" / "distraytracer.h"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["trace.hip", "render_minreg.hip", "photon_build.hip", "cli_loader.cpp", "scene_build.cpp", "photon.cpp"]
 # per-source compiler flags: render_minreg.hip holds C3's and C5's render variants, which run
@@ -25,20 +35,54 @@ HEADERS = ["rt_types.h", "rt_internal.h", "host_math.h", "trace_device.h", "trac
 COMPILE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
                  "-Wall", "-Wno-unused-result", "-Wno-unused-function"]
 
+last_action = None  # "compiled" / "reused" after build()
+
+
+def _extra_flags(src: str, defines: list[str] | None) -> list[str]:
+    """Tuning-build flags for one source: "-..." is a compiler flag, "@<source>:<flag>" a flag
+    for that source only, anything else a -D define. A per-source -D could give the two render
+    translation units different struct layouts or LDS sizes, so it is refused."""
+    out = []
+    for d in defines or []:
+        if d.startswith("@"):
+            s, f = d[1:].split(":", 1)
+            if f.startswith("-D"):
+                raise ValueError(f"per-source defines are not allowed ({d}): both render TUs must agree")
+            out += [f] if s == src else []
+        else:
+            out.append(d if d.startswith("-") else "-D" + d)
+    return out
+
+
+def build_id(defines: list[str] | None = None) -> str:
+    """Hash of the sources, headers and flags a build compiles (16 hex digits)."""
+    h = hashlib.sha256()
+    for p in [CSRC / s for s in SOURCES + HEADERS] + [PUBLIC_HEADER]:
+        h.update(p.name.encode() + b"\0" + p.read_bytes() + b"\0")
+    h.update(json.dumps([COMPILE_FLAGS, SOURCE_FLAGS, sorted(defines or [])]).encode())
+    return h.hexdigest()[:16]
+
+
+def built_id() -> str | None:
+    """The build id recorded for the in-tree library, None if there is none."""
+    try:
+        return json.loads(INFO_PATH.read_text()).get("build_id") if LIB_PATH.exists() else None
+    except (OSError, ValueError):
+        return None
+
 
 def _stale() -> bool:
-    if not LIB_PATH.exists():
-        return True
-    t = LIB_PATH.stat().st_mtime
-    deps = [CSRC / s for s in SOURCES + HEADERS] + [PKG.parent / "include" / "distraytracer.h"]
-    return any(p.stat().st_mtime > t for p in deps)
+    return built_id() != build_id()
 
 
 def build(force: bool = False, verbose: bool = False, defines: list[str] | None = None, out: Path | None = None) -> Path:
     """Build the library (in-tree). `defines`/`out`: tuning experiments (tools/variant_sweep.py)."""
+    global last_action
     target = Path(out) if out else LIB_PATH
     if not force and not defines and out is None and not _stale():
+        last_action = "reused"
         return LIB_PATH
+    bid = build_id(defines)
     target.parent.mkdir(parents=True, exist_ok=True)
     tmp = target.with_suffix(".so.tmp%d" % os.getpid())
     objs, logs = [], []
@@ -46,16 +90,8 @@ def build(force: bool = False, verbose: bool = False, defines: list[str] | None 
     for src in SOURCES:  # .hip -> device+host; .cpp -> host-only C++ (no device pass)
         obj = target.parent / (tag + src + ".o")
         lang = [] if src.endswith(".hip") else ["-x", "c++"]
-        # defines starting with "-" are extra compiler flags, "@<source>:<flag>" a flag for one
-        # source only (tuning experiments)
-        dflags = []
-        for d in defines or []:
-            if d.startswith("@"):
-                s, f = d[1:].split(":", 1)
-                dflags += [f] if s == src else []
-            else:
-                dflags.append(d if d.startswith("-") else "-D" + d)
-        cmd = [HIPCC, *COMPILE_FLAGS, *SOURCE_FLAGS.get(src, []), *dflags, *lang, "-c", str(CSRC / src), "-o", str(obj)]
+        cmd = [HIPCC, *COMPILE_FLAGS, *SOURCE_FLAGS.get(src, []), *_extra_flags(src, defines), f'-DRT_BUILD_ID="{bid}"',
+               *lang, "-c", str(CSRC / src), "-o", str(obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         logs.append(r.stderr)
         if r.returncode != 0:
@@ -67,8 +103,11 @@ def build(force: bool = False, verbose: bool = False, defines: list[str] | None 
     if verbose:
         print("\n".join(logs))
     os.replace(tmp, target)
+    if out is None:
+        INFO_PATH.write_text(json.dumps({"build_id": bid, "defines": defines or []}) + "\n")
+    last_action = "compiled"
     return target
 
 
 if __name__ == "__main__":
-    print(build(force=True))
+    print(build(force=True), last_action, build_id())

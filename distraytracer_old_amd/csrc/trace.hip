@@ -273,6 +273,10 @@ int rt_upload_photons(rt_scene* s) {  // after the host photon-map build (csrc/p
 extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
+#ifndef RT_BUILD_ID
+#define RT_BUILD_ID "unknown"  // set by distraytracer_old_amd/build.py
+#endif
+const char* rt_build_id(void) { return RT_BUILD_ID; }
 const char* rt_last_error(void) { return g_last_error.c_str(); }
 
 int rt_device_count(int* count) {
@@ -354,6 +358,10 @@ static int make_params(rt_scene* s, const rt_render_params* p, ParamsD& P) {
   P.H = p->height;
   P.spp = p->spp > 0 ? p->spp : s->hs.rpp;
   if (P.spp <= 0) return set_error(RT_E_INVALID, "rays_per_pixel is 0 (scene has no fov/rays_per_pixel; Q26)");
+  // the compacted shadow rays hand a shading lane's RNG key to another lane packed in 64 bits
+  // (dv::key_pack): pixel index < 2^32, sample < 2^20
+  if ((int64_t)P.W * P.H > (int64_t)UINT32_MAX || P.spp >= (1 << 20))
+    return set_error(RT_E_INVALID, "image larger than 2^32 pixels or spp >= 2^20");
   const int band = p->row_band <= 1 ? 1 : p->row_band;
   P.row0 = p->row0;
   P.rowStep = step;
@@ -441,8 +449,23 @@ static const Variant kVariants[] = {
     {dv::FT_ALL, dv::render_kernel<false, dv::FT_ALL>},
 };
 
+// RT_RENDER_SHCOMPACT: the same variants with the wave's shadow rays traced compacted
+// (render_kernel<..., true>); the ones the benchmark configs run, and the generic one
+static const Variant kVariantsShc[] = {
+    {0u, dv::render_kernel<false, 0u, true>},
+    {dv::FT_PRIM | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX,
+     dv::render_kernel<false, dv::FT_PRIM | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX, true>},
+    {dv::FT_PRIM | dv::FT_TRANS | dv::FT_PHOTON | dv::FT_LIGHTX,
+     dv::render_kernel<false, dv::FT_PRIM | dv::FT_TRANS | dv::FT_PHOTON | dv::FT_LIGHTX, true>},
+    {dv::FT_ALL, dv::render_kernel<false, dv::FT_ALL, true>},
+};
+
 static RenderFn pick_variant(const HostScene& h, uint32_t flags) {
   uint32_t f = (flags & RT_RENDER_GENERIC) ? (uint32_t)dv::FT_ALL : scene_features(h);
+  if (flags & RT_RENDER_SHCOMPACT) {
+    for (const Variant& v : kVariantsShc)
+      if ((f & ~v.mask) == 0) return v.fn;
+  }
   for (const Variant& v : kVariants)
     if ((f & ~v.mask) == 0) return v.fn;
   return dv::render_kernel<false, dv::FT_ALL>;

@@ -301,7 +301,10 @@ static constexpr int LDS_BYTES = LDS_BASE_BYTES;
 // render kernel: + the per-pixel colour sums of a multi-round sample loop (G >= 2: at most 32
 // pixels per wave), kept in LDS across the shading trees instead of in VGPRs
 static constexpr int SUM_BYTES = 32 * 3 * 8;
-static constexpr int LDS_RENDER_BYTES = LDS_BYTES + SUM_BYTES;
+// + the lane masks of one group of lights whose shadow rays are traced compacted (light_sum_w)
+static constexpr int GRP_MAX = 8;
+static constexpr int GRP_BYTES = GRP_MAX * 8;
+static constexpr int LDS_RENDER_BYTES = LDS_BYTES + SUM_BYTES + GRP_BYTES;
 static_assert(16 * LDS_RENDER_BYTES <= 160 * 1024, "16 waves per CU");
 typedef __attribute__((address_space(3))) double lds_f64;
 typedef __attribute__((address_space(3))) int32_t lds_i32;
@@ -419,7 +422,10 @@ DEVI lds_u64* pkM() { return (lds_u64*)(pkB() + PKO_M); }
 // read come from LDS.
 // slots: while light_sum runs -- the node's ambient (+ photon) colour, ltMult, texture colour,
 // normal, view direction, light sums; between two rays of a shading tree -- the next ray.
-enum { SL_BASE = 0, SL_LTM = 3, SL_TEX = 4, SL_NRM = 7, SL_DW = 10, SL_RGB = 13, SL_N = 16, SL_RAYO = 0, SL_RAYD = 3 };
+// With compacted shadow rays (light_sum_w) the light sums stay in registers and slots 3 / 13..15
+// hold the hit's RNG key and point, which the lanes tracing its shadow rays read.
+enum { SL_BASE = 0, SL_LTM = 3, SL_TEX = 4, SL_NRM = 7, SL_DW = 10, SL_RGB = 13, SL_N = 16, SL_RAYO = 0, SL_RAYD = 3,
+       SL_KEY = 3, SL_FWD = 13 };
 DEVI void stash(int q, double v) { pkT()[q * 64 + __lane_id()] = v; }
 DEVI double unstash(int q) { return pkT()[q * 64 + __lane_id()]; }
 DEVI void stash3(int q, V v) { stash(q, v.x); stash(q + 1, v.y); stash(q + 2, v.z); }
@@ -2208,6 +2214,397 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Compacted shadow rays (packet kernels). calcShadowColor (myObjShader.java:98-153) traces one
+// shadow ray per light for the hit being shaded. Lane by lane (trace_sample / light_sum), a
+// light's shadow rays are traced by the lanes that hit something in this step of their own
+// shading tree and whose spot cone holds the point (ltMult != 0): in C4 an any-hit step ran
+// with 32 % of its lanes. Here the whole wave runs every shading step together
+// (trace_sample_w), and the (lane, light) pairs with a shadow ray are numbered by ballot +
+// prefix count -- light-major, lanes in order -- so that lane e of the wave traces pair e, up
+// to 64 pairs per pass. Each pair's outcome (blocked, or how many in-place re-normalisations
+// its direction went through, myRay.java:93) goes back to the shading lane by ds_bpermute, and
+// that lane adds the light's terms in light order from the same operands as light_sum: the
+// image is bit-identical to the lane-by-lane loop (and so are the instrumented counters).
+// Selected per render by RT_RENDER_SHCOMPACT (render_kernel<..., SHC = true>): measured on
+// MI355X it is bit-identical but slower on C3 / C4 / C5 (DESIGN.md §4 "Compacted shadow rays"),
+// so it is not the default.
+DEVI lds_u64* grpM() { return (lds_u64*)(pkB() + LDS_BYTES + SUM_BYTES); }
+DEVI uint64_t lanes_below() {
+  const int l = __lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+// position of the r-th (0-based) set bit of m, r < popcount(m)
+DEVI int nth_bit(uint64_t m, int r) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const int c = __popcll(m & ((1ull << w) - 1));
+    if (r >= c) { r -= c; m >>= w; pos += w; }
+  }
+  return pos;
+}
+// the RNG key of a shading lane, for the lane tracing its shadow ray (pixel < 2^32, sample <
+// 2^20, node < 2^12: checked by the host)
+DEVI double key_pack(const Key& k) {
+  return __builtin_bit_cast(double, (uint64_t)(uint32_t)k.pixel | ((uint64_t)(k.sample & 0xFFFFFu) << 32) |
+                                        ((uint64_t)(k.node & 0xFFFu) << 52));
+}
+DEVI Key key_unpack(double v, uint64_t seed, uint32_t tsite) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  Key k;
+  k.seed = seed; k.pixel = (uint32_t)b; k.sample = (uint32_t)(b >> 32) & 0xFFFFFu; k.node = (uint32_t)(b >> 52);
+  k.tsite = tsite;
+  return k;
+}
+// the shadow ray of light li from the hit point fwd, as light_sum sets it up
+// (calcShadowColor :98-121): direction, distance to the light, spot fall-off.
+// U: li is wave-uniform (the light record as scalar loads)
+struct ShRay {
+  V d;
+  double dist, ltm;
+};
+template <uint32_t F, bool U>
+DEVI ShRay shadow_ray(const SceneD& S, int li, V fwd, const Key& k) {
+  const LightD& L = S.light[li];
+  auto ld = [&](const double* p) { return U ? sload(p) : *p; };
+  const int32_t ltype = U ? sload(&L.type) : L.type;
+  double lg[12];
+#pragma unroll
+  for (int q = 0; q < 12; ++q) lg[q] = ld(L.g + q);
+  const V lorg = mk(ld(L.origin), ld(L.origin + 1), ld(L.origin + 2));
+  const bool disk = (F & FT_LIGHTX) && ltype == 2;
+  const V lo = disk ? disk_pos(L, k, 0) : lorg;
+  V ln = xpt(lg, lo);
+  ln = nrmz(mk(ln.x - fwd.x, ln.y - fwd.y, ln.z - fwd.z));
+  ShRay r;
+  r.d = nrmz(ln);  // myRay ctor normalises again
+  const V lo2 = disk ? disk_pos(L, k, 2) : lorg;
+  r.dist = sqrt((((fwd.x - lo2.x) * (fwd.x - lo2.x)) + ((fwd.y - lo2.y) * (fwd.y - lo2.y))) +
+                ((fwd.z - lo2.z) * (fwd.z - lo2.z)));
+  r.ltm = 1;
+  if ((F & FT_LIGHTX) && ltype == 1) {  // mySpotLight.calcT_Mult (myLight.java:77-82,159-163)
+    const double angle = jf::acos(-1 * dot(r.d, ld3(L.orient)));
+    r.ltm = (angle < L.innerRad) ? 1 : (angle > L.outerRad) ? 0 : (L.outerRad - angle) / L.radDiff;
+  }
+  return r;
+}
+// calcShadowColor for the hits of one wave step. Every lane of the wave calls it; `hit`: this
+// lane shades a hit whose point, key, normal, view direction and texture colour are in the
+// stash slots (shade_pre). Returns the lane's light sum (light_sum's value).
+template <bool CNT, uint32_t F>
+DEVI V light_sum_w(const SceneD& S, bool hit, int32_t mat, const Key& k, Counters& ct) {
+  if (!__ballot(hit)) return mk(0, 0, 0);
+  const int lane = __lane_id();
+  double r = 0, g = 0, b = 0;
+  lds_u64* gm = grpM();
+  int li0 = 0, ns = 0, n = 0;  // the pending group: lights li0 .. li0 + ns - 1 with n shadow rays
+  const int nl = S.nlight;
+  for (int li = 0; li <= nl; ++li) {
+    uint64_t mask = 0;
+    if (li < nl) {  // pass 1: which lanes have a shadow ray for light li
+      double ltm = 0;
+      if (hit) {
+        if (CNT) ct.c[C_LIGHT]++;
+        ltm = shadow_ray<F, true>(S, li, unstash3(SL_FWD), k).ltm;
+        if (CNT && ltm != 0) ct.c[C_SHADOW]++;
+      }
+      WCNT(C_WLIGHT, 1);  // the light record: scalar loads, once per wave
+      mask = __ballot(hit && ltm != 0);
+    }
+    const int c = __popcll(mask);
+    if (li == nl || n + c > 64 || ns == GRP_MAX) {
+      if (n > 0) {
+        lds_barrier();
+        // pass 2: lane e traces the group's e-th shadow ray (source lane, light) -> res
+        int es = 0, er = 0, base = 0;
+        for (int s = 0; s < ns; ++s) {
+          const int cs = __popcll(uni64(gm[s]));
+          if (lane >= base && lane < base + cs) { es = s; er = lane - base; }
+          base += cs;
+        }
+        int res = -1;  // -1: blocked (or no ray); else the re-normalisations of its direction
+        if (lane < n) {
+          const int src = nth_bit(gm[es], er);
+          const V o = mk(pkT()[SL_FWD * 64 + src], pkT()[(SL_FWD + 1) * 64 + src], pkT()[(SL_FWD + 2) * 64 + src]);
+          const Key sk = key_unpack(pkT()[SL_KEY * 64 + src], k.seed, SITE_SHADOW_TIME + li0 + es);
+          const ShRay sh = shadow_ray<F, false>(S, li0 + es, o, sk);
+          WRay sr;
+          sr.o = o; sr.d = sh.d; sr.d0 = sh.d; sr.stable = false; sr.moved = false; sr.ver = 0;
+          PKSTAT(P_SH_STEP, __ballot(1));
+          PROF_T0(t_shd);
+#ifdef RT_PROF_NOSHADOW  // profiling builds only (tools/variant_sweep.py): results differ
+          if (true) {
+#else
+          if (!shadowed<CNT, F, PACKET>(S, sr, sk, sh.dist, ct)) {
+#endif
+            renorm(sr);  // shadowRay.direction._normalize()
+            res = (int)sr.ver;
+          }
+          PROF_ADD(t_shd, R_SHADOW);
+        }
+        lds_barrier();
+        // pass 3: each shading lane adds its lights' terms, in light order (light_sum)
+        const uint64_t below = lanes_below();
+        base = 0;
+        for (int s = 0; s < ns; ++s) {
+          const uint64_t m = uni64(gm[s]);
+          const int rs = __builtin_amdgcn_ds_bpermute((base + (int)__popcll(m & below)) << 2, res);
+          base += __popcll(m);
+          if (in_mask(m) && rs >= 0) {
+            const int lj = li0 + s;
+            const ShRay sh = shadow_ray<F, true>(S, lj, unstash3(SL_FWD), k);
+            V d = sh.d;  // the direction after the scan's re-normalisations: nrmz^rs(d0)
+            for (int q = 0; q < rs; ++q) d = nrmz(d);
+            const LightD& L = S.light[lj];
+            const V lcol = mk(sload(L.color), sload(L.color + 1), sload(L.color + 2));
+            const V hn = unstash3(SL_NRM);
+            const double ldp = dot(d, hn) * sh.ltm;
+            if (ldp > EPS) {
+              const V tx = unstash3(SL_TEX);
+              r += tx.x * lcol.x * ldp;
+              g += tx.y * lcol.y * ldp;
+              b += tx.z * lcol.z * ldp;
+            }
+#ifndef RT_PROF_NOPHONG  // profiling builds only: results differ
+            const MatD& mt = S.mat[mat];
+            if (mt.phong != 0) {  // the specular term at shading precision (light_sum)
+              const V hdw = unstash3(SL_DW);
+              const V hv = mk(d.x - hdw.x, d.y - hdw.y, d.z - hdw.z);
+              const double hm = mag(hv), hr = hm == 0 ? 1.0 : 1.0 / hm;
+              const double hdp = (hv.x * hr * hn.x + hv.y * hr * hn.y + hv.z * hr * hn.z) * sh.ltm;
+              if (hdp > EPS) {
+                const double ph = pow_shade(hdp * hdp, mt.phong);
+                r += mt.specular[0] * lcol.x * ph;
+                g += mt.specular[1] * lcol.y * ph;
+                b += mt.specular[2] * lcol.z * ph;
+              }
+            }
+#endif
+          }
+        }
+        lds_barrier();
+      }
+      li0 = li; ns = 0; n = 0;
+    }
+    if (li < nl) {
+      gm[ns] = mask;  // wave-uniform: every lane writes the same value
+      ns++;
+      n += c;
+    }
+  }
+  return mk(r, g, b);
+}
+
+// getColorAtPos (myObjShader.java:409-438) around the wave's compacted shadow rays.
+// shade_pre: the hit's ambient (+ photon) and texture colours; what the light terms and the
+// lanes tracing its shadow rays need goes to the stash slots.
+template <bool CNT, uint32_t F>
+DEVI void shade_pre(const SceneD& S, const HitRec& h, const Key& k, Counters& ct) {
+  const MatD& m = S.mat[h.mat];
+  double r = m.ambient[0], g = m.ambient[1], b = m.ambient[2];
+  if constexpr ((F & FT_PHOTON) != 0) {
+    if (!m.simple && (m.krefl == 0.0) && m.usePhotonMap) {
+#ifdef RT_PROF_NOGATHER  // profiling builds only: results differ
+      V ir = mk(0, 0, 0);
+#else
+      PROF_T0(t_ph);
+      V ir = irradiance<CNT>(S, h.fwd, ct);
+      PROF_ADD(t_ph, R_PHOTON);
+#endif
+      if (m.isCausticPhtn) { r += ir.x; g += ir.y; b += ir.z; }
+      else { r += m.diffuse[0] * ir.x; g += m.diffuse[1] * ir.y; b += m.diffuse[2] * ir.z; }
+    }
+  }
+  PROF_T0(t_tex);
+  const V tex = diff_color<CNT, F>(S, m, h, k, m.simple ? 1.0 : m.diffConst, ct);
+  PROF_ADD(t_tex, R_TEX);
+  stash3(SL_BASE, mk(r, g, b)); stash3(SL_TEX, tex); stash3(SL_NRM, h.nrm); stash3(SL_DW, h.dw);
+  stash3(SL_FWD, h.fwd); stash(SL_KEY, key_pack(k));
+  lds_barrier();
+}
+// shade_post: the node's colour (ambient + photon + light sum) and its children, as shade_node
+// after light_sum; the hit's point, normal and view direction come from the stash slots
+template <bool CNT, uint32_t F>
+DEVI int shade_post(const SceneD& S, int32_t mat, V ls, const Child& in, FrameOf<F>& Fr, Child& a, bool& branch,
+                    Counters& ct) {
+  const MatD& m = S.mat[mat];
+  lds_barrier();
+  const V base = unstash3(SL_BASE);
+  Fr.local = mk(base.x + ls.x, base.y + ls.y, base.z + ls.z);
+  branch = (in.gen < S.numRays - 2) && m.hasCaustic;
+#ifdef RT_PROF_NOSECONDARY  // profiling builds only: results differ
+  branch = false;
+#endif
+  if (!branch) return 0;
+  HitRec hs;
+  hs.nrm = unstash3(SL_NRM);
+  hs.dw = unstash3(SL_DW);
+  const V fwd = unstash3(SL_FWD);
+  lds_barrier();
+  a.o = fwd;
+  stash3(SL_RAYO, a.o);  // the child ray goes to trace_sample_w through LDS
+  a.gen = in.gen + 1;
+  a.node = in.node * 2;
+  if constexpr ((F & FT_TRANS) != 0) {
+    bool trans = !m.simple && ((m.ktrans > 0) || (m.perm > 0.0));
+    bool strans = m.simple && (m.ktrans > 0);
+    if (trans || strans) {  // calcTransClr :157-276 / calcSimpleTransClr :503-631
+      double ik[2];
+      kt_of(S, in.ktm, ik);
+      const TransOut T = trans_split(m, hs, ik, strans);
+      Fr.mat = mat;
+      Fr.mode = strans ? FM_SIMPLE : FM_FRESNEL;
+      Fr.wa = T.omtr;
+      Fr.wb = T.tr;
+      if (T.doA) {
+        a.d = T.refr;
+        stash3(SL_RAYD, a.d);
+        a.ktm = mat;
+        if (CNT) ct.c[C_REFR]++;
+        Fr.phase = 1;
+        Fr.hasB = T.doB;
+        if (T.doB) {
+          Fr.dB = T.refl;
+          Fr.org = fwd;
+          Fr.node = in.node;
+          Fr.gen = in.gen;
+        }
+        return T.doB ? 2 : 1;
+      }
+      if (T.doB) {  // only the reflection child: spawn it as "B"
+        a.d = T.refl;
+        stash3(SL_RAYD, a.d);
+        a.node = in.node * 2 + 1;
+        a.ktm = strans ? -1 : mat;
+        if (CNT) ct.c[C_REFL]++;
+        Fr.phase = 3;
+        return 1;
+      }
+      return 0;
+    }
+  }
+  if (m.krefl > 0.0) {  // calcReflClr :278-294
+    V back = mk(hs.dw.x * -1, hs.dw.y * -1, hs.dw.z * -1);
+    V rd = refl_dir(back, hs.nrm);
+    if (dot(rd, hs.nrm) >= 0) {
+      a.d = rd;
+      stash3(SL_RAYD, a.d);
+      a.ktm = -1;
+      Fr.phase = 1;
+      Fr.mat = mat;
+      if constexpr ((F & FT_TRANS) != 0) {
+        Fr.mode = FM_REFL;
+        Fr.hasB = 0;
+      }
+      if (CNT) ct.c[C_REFL]++;
+      return 1;
+    }
+  }
+  return 0;
+}
+
+// trace_sample with the whole wave in step: every lane runs the loop until no lane of the wave
+// has a ray left (`live`), so all 64 lanes reach light_sum_w together and can trace the step's
+// shadow rays. Same shading tree, order and arithmetic per lane as trace_sample.
+template <bool CNT, uint32_t F>
+DEVI V trace_sample_w(const SceneD& S, V org, V dir, Key k, bool live, Counters& ct) {
+  FrameOf<F> fr[MAX_FRAMES];
+  int sp = 0;
+  Child in;
+  in.o = org; in.d = dir; in.node = 1; in.gen = 0; in.ktm = -1;
+  V out = mk(0, 0, 0);
+  if (live) { stash3(SL_RAYO, in.o); stash3(SL_RAYD, in.d); }
+  while (__ballot(live)) {
+    bool hit = false;
+    int32_t mat = 0;
+    V c = mk(0, 0, 0);
+    if (live) {
+      lds_barrier();
+      in.o = unstash3(SL_RAYO); in.d = unstash3(SL_RAYD);
+      WRay w;
+      w.o = in.o; w.d = nrmz(in.d); w.d0 = w.d; w.stable = false; w.moved = false; w.ver = 0;  // myRay ctor
+      k.node = in.node;
+      PKSTAT(P_RAY_STEP, __ballot(1));
+      const Best bh = closest<CNT, F, PACKET>(S, w, k, ct);
+      if (bh.t == DMAX) {
+        PROF_T0(t_bg);
+        c = background<CNT, F>(S, w, ct);
+        PROF_ADD(t_bg, R_BG);
+      } else {
+        PROF_T0(t_hit);
+        const HitRec h = make_hit<F>(S, bh, w, k);
+        PROF_ADD(t_hit, R_HIT);
+        PROF_T0(t_sh);
+        shade_pre<CNT, F>(S, h, k, ct);
+        PROF_ADD(t_sh, R_SHADE);
+        mat = h.mat;
+        hit = true;
+      }
+    }
+    PROF_T0(t_ls);
+    const V ls = light_sum_w<CNT, F>(S, hit, mat, k, ct);
+    PROF_ADD(t_ls, R_LIGHT);
+    if (live) {
+      bool spawned = false;
+      if (hit) {
+        bool branch;
+        Child a;
+        FrameOf<F>& Fr = fr[sp];
+        const int nch = shade_post<CNT, F>(S, mat, ls, in, Fr, a, branch, ct);
+        if (nch > 0 && sp < MAX_FRAMES) {
+          sp++;
+          in = a;  // its o / d are in the LDS slots (shade_post)
+          spawned = true;
+        } else {
+          c = branch ? clampc(add(Fr.local, mk(0, 0, 0))) : clampc(Fr.local);  // no child: acc stayed 0
+        }
+      }
+      // deliver finished colours upward (trace_sample)
+      while (!spawned && sp > 0) {
+        FrameOf<F>& P = fr[sp - 1];
+        if constexpr ((F & FT_TRANS) == 0) {  // the only child has returned
+          const double* wA = S.mat[P.mat].kreflclr;
+          V acc = mk(0 + (wA[0] * c.x), 0 + (wA[1] * c.y), 0 + (wA[2] * c.z));
+          c = clampc(add(P.local, acc));
+          sp--;
+        } else {
+          const MatD& m = S.mat[P.mat];
+          const uint8_t ph = P.phase, mode = P.mode;
+          V acc;
+          if (ph == 1) {
+            V wA;
+            if (mode == FM_REFL) wA = mk(m.kreflclr[0], m.kreflclr[1], m.kreflclr[2]);
+            else if (mode == FM_SIMPLE) { const double w = P.wa * m.ktrans; wA = mk(w, w, w); }
+            else wA = mk(P.wa * m.permclr[0], P.wa * m.permclr[1], P.wa * m.permclr[2]);
+            acc = mk(0 + (wA.x * c.x), 0 + (wA.y * c.y), 0 + (wA.z * c.z));
+            if (P.hasB) {  // second child (Fresnel reflection)
+              P.phase = 2;
+              P.acc = acc;
+              in.o = P.org; in.d = P.dB; in.gen = P.gen + 1; in.node = P.node * 2 + 1;
+              in.ktm = (mode == FM_SIMPLE) ? -1 : P.mat;
+              stash3(SL_RAYO, in.o); stash3(SL_RAYD, in.d);
+              if (CNT) ct.c[C_REFL]++;
+              spawned = true;
+              break;
+            }
+          } else {
+            V wB;
+            if (mode == FM_SIMPLE) { const double w = P.wb * m.krefl; wB = mk(w, w, w); }
+            else wB = mk(P.wb * m.permclr[0], P.wb * m.permclr[1], P.wb * m.permclr[2]);
+            const V a0 = (ph == 2) ? P.acc : mk(0, 0, 0);
+            acc = mk(a0.x + (wB.x * c.x), a0.y + (wB.y * c.y), a0.z + (wB.z * c.z));
+          }
+          c = clampc(add(P.local, acc));
+          sp--;
+        }
+      }
+      if (!spawned) { out = c; live = false; }
+    }
+  }
+  return out;
+}
+
 // XCD-aware tile order. Workgroups are dealt round-robin to the 8 XCDs (block b -> XCD
 // b % 8), each with its own L2. With XCD_CHUNKS = k > 0 the row-major tile list is cut
 // into 8k contiguous chunks and XCD x renders chunks x, x+8, ...: each L2 then sees a
@@ -2269,9 +2666,12 @@ __device__ unsigned long long* rt_tl_buf;
 #define RT_SPLIT_TU 1
 #endif
 static constexpr uint32_t F_C5 = FT_PRIM | FT_TRANS | FT_PHOTON | FT_LIGHTX;
-template <bool CNT, uint32_t F>
+// SHC: the shading steps of a wave run in step and their shadow rays are traced compacted
+// (trace_sample_w / light_sum_w) instead of lane by lane (trace_sample)
+template <bool CNT, uint32_t F, bool SHC = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_RENDER_WAVES)))
 render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict__ argb, unsigned long long* __restrict__ gcount) {
+  constexpr bool SH_COMPACT = SHC && STASH_SHADE;
   // One wave = a tw x th pixel tile x G sample lanes per pixel. Samples of one pixel are
   // nearly the same ray, so the G lanes of a pixel traverse the same nodes (coherent
   // loads, little divergence). Lane j of a pixel traces samples j, j+G, ...; each round's
@@ -2337,8 +2737,8 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
     const int s = s0 + j;
     V cc = mk(0, 0, 0);
     bool traced = false;  // a fisheye sample outside the image circle adds nothing (myScene.java:1571)
+    V o = mk(0, 0, 0), d = mk(0, 0, 0);
     if (valid && s < n) {
-      V o, d;
       traced = true;
       if ((F & FT_CAMX) && P.cam == 1) {  // myFishEyeScene: draw (1 spp) :1605-1622 / shootMultiRays :1562-1583
         double xVal, yVal, rSq;
@@ -2386,7 +2786,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
         o = mk(0, 0, 0);
         d = mk(rx, ry, P.viewZ);
       }
-      if (traced) {
+      if (!SH_COMPACT && traced) {
         Key ks = k;
         ks.sample = (uint32_t)s;
         if (CNT) ct.c[C_CAMERA]++;
@@ -2394,6 +2794,14 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
         cc = trace_sample<CNT, F>(S, o, d, ks, ct);
         PROF_ADD(t_smp, R_SAMPLE);
       }
+    }
+    if constexpr (SH_COMPACT) {  // every lane of the wave: the shading steps run in step
+      Key ks = k;
+      ks.sample = (uint32_t)s;
+      if (CNT && traced) ct.c[C_CAMERA]++;
+      PROF_T0(t_smp);
+      cc = trace_sample_w<CNT, F>(S, o, d, ks, traced, ct);
+      PROF_ADD(t_smp, R_SAMPLE);
     }
     if (G == 1) {  // one sample per pixel (G = 1 only for spp = 1): one round
       if constexpr (SUMS_LDS) {  // its colour waits in cbuf

@@ -70,6 +70,10 @@ class FrameExchange:
       ex = FrameExchange(dist, H, (maxrows, W, 3), device)
       for each frame: ex.step(lambda tile: render into tile)
       ex.finish()                      # ex.image: the last assembled frame (rank 0)
+
+    `step` is `tile()` (this frame's buffer), the render, then `post()` (complete the previous
+    frame, start this one's gather): several exchanges (e.g. float RGB and ARGB planes) can share
+    one render that way.
     """
 
     def __init__(self, dist, H: int, tile_shape, device, dtype=None, band: int = BAND):
@@ -92,12 +96,21 @@ class FrameExchange:
             if self.rank == 0:
                 self.image.copy_(assemble(self.gathered, self.H, self.band))
 
-    def step(self, render):
-        tile = self.tiles[self.frame % 2]
-        render(tile)  # enqueued before the previous frame's gather is waited for: they overlap
-        self._complete()  # frame-1 gathered + assembled; its tile buffer is free again
+    def tile(self):
+        """This frame's tile buffer (render into it, then post())."""
+        return self.tiles[self.frame % 2]
+
+    def post(self):
+        """Complete frame-1 (gathered + assembled; its buffer is free again) and start this
+        frame's gather. The render was enqueued before the wait: the two overlap."""
+        tile = self.tile()
+        self._complete()
         self._pending = self._gather(tile)
         self.frame += 1
+
+    def step(self, render):
+        render(self.tile())
+        self.post()
 
     def _gather(self, tile):
         if not getattr(self, "_use_allgather", False):
@@ -186,19 +199,24 @@ def build_photons_sharded(scene, seed: int, count: int, dist=None, device="cuda"
 
 class RankRenderer:
     """One rank's share of bench.py's N-GPU step: renders the rank's row bands (rows_of) with
-    the HIP kernel into a device tile on the current stream (rt_render_device), and with N > 1
-    hands the tile to FrameExchange (gathered to rank 0 and re-interleaved there, pipelined
-    against the next frame). `stage_host`: copy the tile to host memory before the exchange
-    (the gloo backend, which cannot gather device tensors; used to run this exact path as
-    several processes on one GPU).
+    the HIP kernel into device tiles on the current stream (rt_render_device: float RGB and the
+    reference's ARGB ints, myObjShader.java:671), and with N > 1 hands the planes in `planes`
+    to a FrameExchange each (gathered to rank 0 and re-interleaved there, pipelined against the
+    next frame). The ARGB plane is the frame the reference produces (`rndrdImg.pixels`,
+    myScene.java:1171-1177): the kernel packs it from the double colour, so rank 0 receives the
+    1-GPU ints exactly (packing the gathered float RGB again could differ by one in a channel
+    whose double value rounds up to the next float). `stage_host`: copy the tiles to host
+    memory before the exchange (the gloo backend, which cannot gather device tensors; used to run
+    this exact path as several processes on one GPU).
 
       rr = RankRenderer(scene, W, H, spp, seed, dist)
       rr.calibrate()                 # untimed: the layout's tile-schedule calibration renders
       for each frame: rr.step()      # optional (start, end) HIP events around the kernel
-      img = rr.finish()              # rank 0: the last assembled frame [H, W, 3] (device / host)
+      rgb, argb = rr.finish()        # rank 0: the last assembled frame, [H, W, 3] float32 and
+                                     # [H, W] int32 (device / host; None for a plane not exchanged)
     """
 
-    def __init__(self, scene, W, H, spp, seed, dist=None, stage_host=False, band=BAND):
+    def __init__(self, scene, W, H, spp, seed, dist=None, stage_host=False, band=BAND, planes=("rgb", "argb")):
         import torch
 
         from . import rt
@@ -212,18 +230,25 @@ class RankRenderer:
         self.rows = (r0, r1, step, b)
         self.maxrows = max_tile_rows(self.world, H, band)
         assert rt.nrows_of(self.p) <= self.maxrows
+        assert set(planes) <= {"rgb", "argb"} and planes
         self.rgb = torch.empty((self.maxrows, W, 3), dtype=torch.float32, device="cuda")
         self.argb = torch.empty((self.maxrows, W), dtype=torch.int32, device="cuda")
         self.stream = torch.cuda.current_stream()
         self.stage_host = stage_host
-        self.ex = None
+        self.ex = {}
         if dist is not None and self.world > 1:
-            self.ex = FrameExchange(dist, H, (self.maxrows, W, 3), "cpu" if stage_host else "cuda", band=band)
+            dev = "cpu" if stage_host else "cuda"
+            if "rgb" in planes:
+                self.ex["rgb"] = FrameExchange(dist, H, (self.maxrows, W, 3), dev, band=band)
+            if "argb" in planes:
+                self.ex["argb"] = FrameExchange(dist, H, (self.maxrows, W), dev, dtype=torch.int32, band=band)
 
-    def render(self, tile, ev=None):
+    def render(self, rgb=None, argb=None, ev=None):
         if ev:
             ev[0].record(self.stream)
-        self.scene.render_device(self.p, tile.data_ptr(), self.argb.data_ptr(), self.stream.cuda_stream)
+        rgb = self.rgb if rgb is None else rgb
+        argb = self.argb if argb is None else argb
+        self.scene.render_device(self.p, rgb.data_ptr(), argb.data_ptr(), self.stream.cuda_stream)
         if ev:
             ev[1].record(self.stream)
 
@@ -232,22 +257,29 @@ class RankRenderer:
         import torch
 
         for _ in range(n):
-            self.render(self.rgb)
+            self.render()
         torch.cuda.synchronize()
 
     def step(self, ev=None):
-        if self.ex is None:
-            self.render(self.rgb, ev)
-        elif self.stage_host:
-            def render(tile):
-                self.render(self.rgb, ev)
-                tile.copy_(self.rgb)  # device -> host (synchronous), then the gloo gather
-            self.ex.step(render)
+        if not self.ex:
+            self.render(ev=ev)
+            return
+        tiles = {k: e.tile() for k, e in self.ex.items()}
+        if self.stage_host:
+            self.render(ev=ev)
+            for k, t in tiles.items():
+                t.copy_(getattr(self, k))  # device -> host (synchronous), then the gloo gather
         else:
-            self.ex.step(lambda tile: self.render(tile, ev))
+            self.render(tiles.get("rgb"), tiles.get("argb"), ev)
+        for e in self.ex.values():
+            e.post()
 
     def finish(self):
-        """Drain the pipelined exchange; rank 0 gets the assembled image [H, W, 3], others None."""
-        if self.ex is not None:
-            return self.ex.finish()
-        return self.rgb[: self.H] if self.rank == 0 else None
+        """Drain the pipelined exchange; rank 0 gets the assembled frame (rgb [H, W, 3], argb
+        [H, W]; None for a plane not exchanged), the other ranks (None, None)."""
+        if self.ex:
+            out = {k: e.finish() for k, e in self.ex.items()}
+            return out.get("rgb"), out.get("argb")
+        if self.rank != 0:
+            return None, None
+        return self.rgb[: self.H], self.argb[: self.H]

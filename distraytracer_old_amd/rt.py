@@ -40,7 +40,7 @@ class RenderParams(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("flags", ctypes.c_uint32), ("row_band", ctypes.c_int32)]
 
 
-EXPORTS = ["rt_abi_version", "rt_last_error", "rt_device_count", "rt_scene_create", "rt_scene_load_cli",
+EXPORTS = ["rt_abi_version", "rt_build_id", "rt_last_error", "rt_device_count", "rt_scene_create", "rt_scene_load_cli",
            "rt_scene_inspect_cli",
            "rt_scene_info", "rt_scene_destroy", "rt_photons_build", "rt_render", "rt_render_device",
            "rt_render_count", "rt_time_render", "rt_render_pass", "rt_refine_steps", "rt_scene_photons",
@@ -66,6 +66,7 @@ def lib():
             raise RTError(f"{p} is missing: build it with `python -m distraytracer_old_amd.build`")
         L = ctypes.CDLL(str(p))
         L.rt_last_error.restype = ctypes.c_char_p
+        L.rt_build_id.restype = ctypes.c_char_p
         L.rt_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.rt_scene_load_cli.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                         ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(TextureDesc),
@@ -107,6 +108,11 @@ def _name_call(fn, *args) -> str:
     buf = ctypes.create_string_buffer(n + 1)
     fn(*args, buf, n + 1)
     return buf.value.decode()
+
+
+def build_id() -> str:
+    """The loaded library's build id (rt_build_id: hash of its sources and flags, build.py)."""
+    return lib().rt_build_id().decode()
 
 
 def png_name(save_name: str) -> str:
@@ -155,6 +161,7 @@ def inspect_cli(cli: str, scene_dir=SCENE_DIR, textures: dict | None = None) -> 
 RENDER_GENERIC = 1  # RT_RENDER_GENERIC: the all-features kernel instead of the scene-specialised one
 RENDER_ROWMAJOR = 2  # RT_RENDER_ROWMAJOR: row-major tile dispatch instead of the longest-first schedule
 RENDER_NOCULL = 4  # RT_RENDER_NOCULL: no bounding-sphere culling of top-level primitives
+RENDER_SHCOMPACT = 8  # RT_RENDER_SHCOMPACT: a wave's shadow rays traced compacted (same image)
 
 
 def params(W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, flags=0, row_band=1) -> RenderParams:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 enum rt_status {
   RT_OK = 0,
@@ -177,6 +177,10 @@ typedef struct rt_render_params {
 #define RT_RENDER_ROWMAJOR 2u
 /* test every top-level primitive (no bounding-sphere culling): same image, slower */
 #define RT_RENDER_NOCULL 4u
+/* trace the shadow rays of a wave's shading step compacted (ballot + prefix count: lane e traces
+   the e-th (hit, light) pair) instead of light by light on the shading lanes: same image (DESIGN.md
+   §4 "Compacted shadow rays"; slower on the benchmark configs, so not the default) */
+#define RT_RENDER_SHCOMPACT 8u
 
 typedef struct rt_scene rt_scene;
 
@@ -191,6 +195,9 @@ enum {
 };
 
 int rt_abi_version(void);
+/* Provenance (ABI 5): a hash of the sources, headers and compiler flags this library was built
+   from (distraytracer_old_amd/build.py build_id); profiles and bench lines record it. */
+const char* rt_build_id(void);
 const char* rt_last_error(void);
 int rt_device_count(int* count);
 

@@ -26,7 +26,10 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(rt.EXPORTS)
-    assert L.rt_abi_version() == 4
+    assert L.rt_abi_version() == 5
+    # provenance: the library carries the build id of the sources and flags it was built from
+    from distraytracer_old_amd import build
+    assert rt.build_id() == build.built_id() == build.build_id()
 
 
 def test_no_gpu_fails_loudly():

@@ -1,0 +1,72 @@
+"""Full-size GPU properties of the SURVEY 8(d) configs C4 and C5 (BASELINE.json configs[3],
+configs[4]), which the parity tests otherwise cover only at reduced size:
+
+* deterministic: two renders are bit-equal;
+* the N-GPU partition: the eight row-band tiles of an 8-rank split (multigpu.rows_of, the
+  layout bench.py --gpus 8 runs) padded, stacked and re-interleaved with multigpu.assemble
+  equal the 1-GPU frame bit for bit, float RGB and ARGB alike;
+* parity: a row subsample of the full frame against the oracle at the full spp, with the
+  decision-exact bar of tests/parity.py (per-channel |d| <= 1e-4 where decisions agree, 0
+  decision mismatches, ARGB equal).
+
+C4 = data/plnts3ColsBunnies.cli 2048^2 x 64 spp (~0.6 s per GPU frame); C5 = data/t11.cli
+1024^2 x 64 spp at its real photon map (2.68 M photons, k = 200; the oracle gathers over the
+GPU's photon_list, which test_c5_full_prepass_and_k200_gather_parity checks is the oracle's
+own bit for bit).
+"""
+import numpy as np
+import pytest
+
+from distraytracer_old_amd import multigpu, rt, scenes
+from oracle.oracle import OracleScene
+from tests.parity import assert_exact_decisions, compare
+
+pytestmark = pytest.mark.gpu
+
+
+def _split_equals_full(g, W, H, spp, seed, rgb, argb, world=8):
+    maxrows = multigpu.max_tile_rows(world, H)
+    tr = np.zeros((world, maxrows, W, 3), np.float32)
+    ta = np.zeros((world, maxrows, W), np.int32)
+    for r in range(world):
+        r0, r1, step, band = multigpu.rows_of(r, world, H)
+        t, a = g.render(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=step, row_band=band)
+        n = multigpu.tile_rows(r, world, H)
+        assert t.shape[0] == n
+        tr[r, :n], ta[r, :n] = t, a
+    assert np.array_equal(multigpu.assemble(ta, H), argb)
+    assert np.array_equal(multigpu.assemble(tr, H).view(np.uint32), rgb.view(np.uint32))
+
+
+def test_c4_full_size_properties():
+    cli, W, H, spp, seed = scenes.CONFIGS["C4"]
+    scenes.ensure_bun69k()
+    tex = scenes.prepare(cli)
+    g = rt.Scene.load_cli(cli, textures=tex)
+    rgb, argb = g.render(W, H, spp=spp, seed=seed)
+    rgb2, argb2 = g.render(W, H, spp=spp, seed=seed)
+    assert np.array_equal(argb, argb2) and np.array_equal(rgb.view(np.uint32), rgb2.view(np.uint32))
+    assert rgb.min() >= 0 and rgb.max() <= 1.0
+    _split_equals_full(g, W, H, spp, seed, rgb, argb)
+    # oracle rows through the glass bunnies, the columns and the sky (the oracle runs ~3 s a row)
+    o = OracleScene(scenes.SCENE_DIR, cli, tex)
+    for row in (700, 1300, 1900):
+        ro, ao, _ = o.render(W, H, spp=spp, seed=seed, rows=(row, row + 1))
+        assert_exact_decisions(compare(rgb[row:row + 1], argb[row:row + 1], ro, ao))
+
+
+def test_c5_full_size_properties():
+    cli, W, H, spp, seed = scenes.CONFIGS["C5"]
+    g = rt.Scene.load_cli(cli, textures={})
+    g.build_photons(seed)
+    assert g.info()["photons"] > 2_600_000
+    rgb, argb = g.render(W, H, spp=spp, seed=seed)
+    rgb2, argb2 = g.render(W, H, spp=spp, seed=seed)
+    assert np.array_equal(argb, argb2) and np.array_equal(rgb.view(np.uint32), rgb2.view(np.uint32))
+    assert rgb.min() >= 0 and rgb.max() <= 1.0
+    _split_equals_full(g, W, H, spp, seed, rgb, argb)
+    o = OracleScene(scenes.SCENE_DIR, cli)
+    o.set_photons(*g.photons())
+    for row in (100, 400, 640, 900):  # ceiling light, spheres (mirror / glass: caustics), floor
+        ro, ao, _ = o.render(W, H, spp=spp, seed=seed, rows=(row, row + 1))
+        assert_exact_decisions(compare(rgb[row:row + 1], argb[row:row + 1], ro, ao))

@@ -213,6 +213,23 @@ def test_specialised_kernel_equals_generic(cli, W, spp):
     assert np.array_equal(rs.view(np.uint32), rg.view(np.uint32))
 
 
+@pytest.mark.parametrize("cli,W,spp", [("c3_bun69k.cli", 128, 4), ("plnts3ColsBunnies.cli", 96, 4),
+                                       ("p2_t05.cli", 96, 2), ("c3spotLight.cli", 96, 2), ("p2_t03.cli", 96, 2),
+                                       ("c2clear.cli", 96, 1), ("t11.cli", 64, 1), ("p3_t11_sierp.cli", 64, 1)])
+def test_compacted_shadow_rays_render_identically(cli, W, spp):
+    """RT_RENDER_SHCOMPACT (the wave's shading steps in step, its (hit, light) shadow rays
+    numbered by ballot + prefix count and traced one per lane): bit-identical to the lane-by-lane
+    light loop -- point / spot / disk lights, moving spheres (keyed shadow-ray times), glass,
+    photon map, instances -- in the scene's variant and the generic one."""
+    scenes.ensure_bun69k()
+    g = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+    ra, aa = g.render(W, W, spp=spp, seed=SEED)
+    for flags in (rt.RENDER_SHCOMPACT, rt.RENDER_SHCOMPACT | rt.RENDER_GENERIC):
+        rb, ab = g.render(W, W, spp=spp, seed=SEED, flags=flags)
+        assert np.array_equal(aa, ab), flags
+        assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32)), flags
+
+
 def test_photon_shards_merge_to_the_full_prepass(tmp_path):
     """Multi-GPU photon pre-pass (8(e)): shards shot separately and merged in rank order give
     the single-GPU photon_list bit for bit, and the same image."""

@@ -117,6 +117,51 @@ def test_gloo_world3_pipelined_exchange_delivers_every_frame(allgather):
     assert np.array_equal(frames, expect)
 
 
+def _planes_worker(rank, world, port, H, W, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows = torch.tensor(multigpu.image_rows(rank, world, H), dtype=torch.int64)
+    maxrows = multigpu.max_tile_rows(world, H)
+    # RankRenderer's pattern: one render fills the float-RGB and ARGB planes, then each is posted
+    ex = {"rgb": multigpu.FrameExchange(dist, H, (maxrows, W, 3), "cpu"),
+          "argb": multigpu.FrameExchange(dist, H, (maxrows, W), "cpu", dtype=torch.int32)}
+    for f in range(3):
+        t = {k: e.tile() for k, e in ex.items()}
+        t["rgb"].zero_()
+        t["rgb"][: len(rows)] = (rows.to(torch.float32) / 7 + f)[:, None, None]
+        t["argb"].zero_()
+        # ARGB ints as the kernel packs them (alpha 255: negative as int32)
+        t["argb"][: len(rows)] = ((0xFF000000 + rows * 65793 + f) - (1 << 32)).to(torch.int32)[:, None]
+        for e in ex.values():
+            e.post()
+    out = {k: e.finish() for k, e in ex.items()}
+    if rank == 0:
+        q.put((out["rgb"].numpy(), out["argb"].numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_rgb_and_argb_planes():
+    """The N-rank frame's two planes (float RGB and the reference's ARGB ints, myObjShader.java:671)
+    go through their own exchanges after one shared render; rank 0 assembles both exactly."""
+    H, W, world = 40, 2, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_planes_worker, args=(r, world, port, H, W, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    rgb, argb = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    r = np.arange(H)
+    assert np.array_equal(rgb, np.broadcast_to((r.astype(np.float32) / 7 + 2)[:, None, None], (H, W, 3)))
+    expect = ((0xFF000000 + r * 65793 + 2) - (1 << 32)).astype(np.int32)
+    assert argb.dtype == np.int32 and np.array_equal(argb, np.broadcast_to(expect[:, None], (H, W)))
+
+
 def test_assemble_numpy_ragged():
     for H, W, world, band in [(10, 3, 4, 1), (37, 5, 3, 4), (1024, 2, 8, 8), (19, 2, 8, 8)]:
         img = np.arange(H * W).reshape(H, W, 1)

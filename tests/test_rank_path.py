@@ -1,7 +1,8 @@
 """bench.py's N-GPU step path on the HIP kernel (VERDICT r01 Next #2): tools/rank_check.py
 runs multigpu.RankRenderer + FrameExchange (+ the sharded photon pre-pass) as 2 ranks over
-gloo sharing device 0 (tiles staged to host), and as 1 rank; the assembled 2-rank frame must
-equal the 1-rank image bit for bit, and bench.py --gpus 2 must print a 2-rank line.
+gloo sharing device 0 (tiles staged to host), and as 1 rank; the assembled 2-rank frame (float
+RGB and ARGB) must equal the 1-rank image bit for bit, and bench.py --gpus 2 must print a 2-rank
+line.
 
 These tests start child processes, so conftest.py runs them before any test of the session
 touches the GPU in the pytest process (no exec from a GPU-initialised process)."""
@@ -27,7 +28,7 @@ def _port():
 
 
 def _run(args, nproc, tmp, name):
-    out = tmp / f"{name}.npy"
+    out = tmp / f"{name}.npz"
     tool = [str(REPO / "tools" / "rank_check.py"), *args, "--out", str(out)]
     if nproc == 1:
         cmd = [sys.executable, *tool]
@@ -36,7 +37,8 @@ def _run(args, nproc, tmp, name):
                "--master-addr=127.0.0.1", f"--master-port={_port()}", *tool]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    return np.load(out)
+    d = np.load(out)
+    return d["rgb"], d["argb"]
 
 
 @pytest.mark.parametrize("args", [
@@ -44,10 +46,13 @@ def _run(args, nproc, tmp, name):
     ["--cli", "t11.cli", "--size", "96", "--spp", "2", "--seed", str(0x5EED0005)],  # sharded photon pre-pass
 ], ids=["c3", "t11_photons"])
 def test_two_rank_step_equals_one_rank_image(tmp_path, args):
-    one = _run(args, 1, tmp_path, "one")
-    two = _run(args, 2, tmp_path, "two")
+    one, one_argb = _run(args, 1, tmp_path, "one")
+    two, two_argb = _run(args, 2, tmp_path, "two")
     assert one.shape == two.shape
     assert np.array_equal(one.view(np.uint32), two.view(np.uint32))
+    # the reference's output, rndrdImg.pixels (myObjShader.java:671): rank 0's assembled ARGB
+    # frame equals the 1-GPU frame's ints
+    assert one_argb.shape == one.shape[:2] and np.array_equal(one_argb, two_argb)
 
 
 def test_bench_gpus2_prints_a_two_rank_line():

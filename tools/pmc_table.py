@@ -61,7 +61,13 @@ def main():
         der["fp64_tflops_upper"] = flops / (ms / 1e3) / 1e12
         if "SQ_INSTS_VALU" in mean:
             der["fp64_share_of_valu"] = sum(f64.values()) / mean["SQ_INSTS_VALU"]
-    out = {"workload": workload, "counters": mean, "derived": der,
+    try:  # the library the profiled run loaded (the same DISTRAYTRACER_LIB / in-tree library)
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+        from distraytracer_old_amd import rt
+        bid = rt.build_id()
+    except Exception:
+        bid = None
+    out = {"workload": workload, "build_id": bid, "counters": mean, "derived": der,
            # bench.py reads these (per launch of the timed render kernel)
            "hbm_bytes_per_launch": der.get("hbm_read_bytes"), "hbm_write_bytes_per_launch": der.get("hbm_write_bytes"),
            "fp64_flop_per_launch": der.get("fp64_flop_per_launch_upper"), "hbm_kernel": kname,

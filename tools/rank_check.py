@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """bench.py's N-rank step path, run for a check: every rank renders its row bands with the HIP
 kernel (multigpu.RankRenderer -> rt_render_device), the photon pre-pass (photon scenes) is
-sharded over the ranks (multigpu.build_photons_sharded), the float-RGB tiles go through
-multigpu.FrameExchange to rank 0, and rank 0 writes the assembled frame to --out (.npy).
+sharded over the ranks (multigpu.build_photons_sharded), the float-RGB and ARGB tiles go through
+multigpu.FrameExchange to rank 0, and rank 0 writes the assembled frame to --out (.npz: rgb, argb).
 
 Launched under torch.distributed.run; with --backend gloo the ranks may share one GPU (tiles
 staged to host), which is how tests/test_rank_path.py runs it on a one-GPU box. Without
@@ -55,15 +55,16 @@ def main():
     frames = []
     for _ in range(a.frames):
         rr.step()
-        if rr.ex is not None and rr.rank == 0 and rr.ex.frame > 1:
-            frames.append(rr.ex.image.cpu().numpy().copy())  # the previous frame, assembled
-    img = rr.finish()
+        ex = rr.ex.get("rgb") if rr.ex else None
+        if ex is not None and rr.rank == 0 and ex.frame > 1:  # the previous frame, assembled
+            frames.append((ex.image.cpu().numpy().copy(), rr.ex["argb"].image.cpu().numpy().copy()))
+    rgb, argb = rr.finish()
     torch.cuda.synchronize()
     if rr.rank == 0:
-        img = img.cpu().numpy()
-        for f in frames:  # every pipelined frame was delivered whole (same seed: same image)
-            assert np.array_equal(f, img), "a pipelined frame differs from the last"
-        np.save(a.out, img)
+        rgb, argb = rgb.cpu().numpy(), argb.cpu().numpy()
+        for f, fa in frames:  # every pipelined frame was delivered whole (same seed: same image)
+            assert np.array_equal(f, rgb) and np.array_equal(fa, argb), "a pipelined frame differs from the last"
+        np.savez(a.out, rgb=rgb, argb=argb)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
