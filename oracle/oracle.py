@@ -60,6 +60,8 @@ def lib():
         L.oracle_set_photons.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         L.oracle_math_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         L.oracle_camera_hits.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_knn.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p,
+                                 ctypes.c_void_p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -120,6 +122,13 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError("oracle render failed")
         return rgb, argb, dict(zip(ST_NAMES, st[: len(ST_NAMES)].tolist()))
+
+    def knn(self, p, cap: int = 4096):
+        """find_near's neighbourhood of point p: (photon indices in poll order, farthest first; d2)."""
+        idx = np.zeros(cap, dtype=np.int32)
+        d2 = np.zeros(cap, dtype=np.float64)
+        n = lib().oracle_knn(self._h, float(p[0]), float(p[1]), float(p[2]), idx.ctypes.data, d2.ctypes.data, cap)
+        return idx[:min(n, cap)].copy(), d2[:min(n, cap)].copy()
 
     def camera_hits(self, W: int, H: int, threads: int = 0) -> np.ndarray:
         """uint8 [H, W]: 1 where the un-jittered FOV camera ray hits an object, 0 where it

@@ -714,9 +714,51 @@ struct KDTree {
   struct QE {
     double d2;
     int p;
-    bool operator<(const QE& o) const { return d2 < o.d2; }
   };
-  void near_rec(const double pos[3], int ni, std::priority_queue<QE>& q, double& max_d2, uint64_t* st) const {  // :408-445
+  // java.util.PriorityQueue<myPhoton>(n, Collections.reverseOrder()) as JDK 8 implements it
+  // (offer -> siftUpUsingComparator, poll -> siftDownUsingComparator; the comparator is
+  // myPhoton.compareTo on pos[3] = d2, reversed: a max-heap). An element moves up only past a
+  // STRICTLY smaller parent and down only past a STRICTLY larger child (the right child only when
+  // strictly larger than the left), so among photons of equal d2 the one poll() evicts and the
+  // poll order of the sum are Java's -- std::priority_queue's sifts break ties differently.
+  struct JavaMaxPQ {
+    std::vector<QE> q;
+    size_t size() const { return q.size(); }
+    bool empty() const { return q.empty(); }
+    const QE& peek() const { return q[0]; }
+    void add(const QE& x) {  // offer + siftUp
+      size_t k = q.size();
+      q.push_back(x);
+      while (k > 0) {
+        const size_t parent = (k - 1) >> 1;
+        if (q[parent].d2 >= x.d2) break;  // reverseOrder.compare(x, e) >= 0
+        q[k] = q[parent];
+        k = parent;
+      }
+      q[k] = x;
+    }
+    QE poll() {  // the root; the last element sifts down from the root
+      const QE r = q[0];
+      const QE x = q.back();
+      q.pop_back();
+      const size_t n = q.size();
+      if (n > 0) {
+        size_t k = 0;
+        const size_t half = n >> 1;
+        while (k < half) {
+          size_t child = 2 * k + 1;
+          const size_t right = child + 1;
+          if (right < n && q[right].d2 > q[child].d2) child = right;  // compare(c, right) > 0
+          if (x.d2 >= q[child].d2) break;                              // compare(x, c) <= 0
+          q[k] = q[child];
+          k = child;
+        }
+        q[k] = x;
+      }
+      return r;
+    }
+  };
+  void near_rec(const double pos[3], int ni, JavaMaxPQ& q, double& max_d2, uint64_t* st) const {  // :408-445
     const KDNode& n = nodes[ni];
     const Photon& ph = photons[n.photon];
     if (st) st[ST_PHOTON]++;
@@ -733,28 +775,32 @@ struct KDTree {
     double dx = pos[0] - ph.pos[0], dy = pos[1] - ph.pos[1], dz = pos[2] - ph.pos[2];
     double len2 = dx * dx + dy * dy + dz * dz;
     if (len2 < max_d2) {
-      q.push(QE{len2, n.photon});
-      if ((int)q.size() > maxNear) q.pop();
+      q.add(QE{len2, n.photon});
+      if ((int)q.size() > maxNear) q.poll();  // delete the most distant photon
       if ((int)q.size() == maxNear) {
-        if (q.top().d2 < max_d2) max_d2 = q.top().d2;
+        if (q.peek().d2 < max_d2) max_d2 = q.peek().d2;
       }
     }
+  }
+  // find_near (:389-405): the neighbourhood in poll order (farthest first)
+  void find_near(const V3& p, std::vector<QE>& out, uint64_t* st) const {
+    out.clear();
+    if (root < 0) return;
+    JavaMaxPQ q;
+    double max_d2 = baseMaxDist2;
+    const double pos[3] = {p.x, p.y, p.z};
+    near_rec(pos, root, q, max_d2, st);
+    while (!q.empty()) out.push_back(q.poll());
   }
   // getIrradianceFromPhtnTree (myObjShader.java:441-458)
   void irradiance(const V3& p, double res[3], uint64_t* st) const {
     res[0] = res[1] = res[2] = 0;
-    if (root < 0) return;
-    std::priority_queue<QE> q;
-    double max_d2 = baseMaxDist2;
-    double pos[3] = {p.x, p.y, p.z};
-    near_rec(pos, root, q, max_d2, st);
-    if (q.empty()) return;  // [null] -> zero (Q20)
-    double rSq = q.top().d2;
-    double area = PI_F * rSq;
-    // the reference sums in poll order (farthest first)
     std::vector<QE> order;
-    while (!q.empty()) { order.push_back(q.top()); q.pop(); }
-    for (const QE& e : order) {
+    find_near(p, order, st);
+    if (order.empty()) return;  // [null] -> zero (Q20)
+    double rSq = order[0].d2;   // hood.get(0): the farthest
+    double area = PI_F * rSq;
+    for (const QE& e : order) {  // the reference sums in poll order (farthest first)
       res[0] += photons[e.p].pwr[0];
       res[1] += photons[e.p].pwr[1];
       res[2] += photons[e.p].pwr[2];
@@ -2387,6 +2433,17 @@ int oracle_set_photons(void* p, const double* pos, const double* pwr, int64_t n)
   T.build_all();
   s->photonsBuilt = true;
   return 0;
+}
+
+// The photon neighbourhood find_near returns for a point (myKD_Tree.find_near, myLight.java:389-445):
+// up to cap photon indices (photon_list order) in poll order, farthest first, and their d2; returns
+// the neighbourhood's size. Tests check the JDK 8 PriorityQueue tie rules on it.
+int oracle_knn(void* p, double x, double y, double z, int32_t* idx, double* d2, int cap) {
+  Scene* s = (Scene*)p;
+  std::vector<KDTree::QE> out;
+  s->photonTree.find_near(V3(x, y, z), out, nullptr);
+  for (int i = 0; i < (int)out.size() && i < cap; ++i) { idx[i] = out[i].p; d2[i] = out[i].d2; }
+  return (int)out.size();
 }
 
 // fdlibm sin / cos / asin / acos (jfdlibm.h, shared with the device) of x[0..n) -> out[4*i..4*i+3]
