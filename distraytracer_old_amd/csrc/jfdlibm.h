@@ -8,7 +8,7 @@
 // Restated from the published fdlibm 5.3 algorithms (k_sin.c, k_cos.c, e_rem_pio2.c,
 // s_sin.c, s_cos.c, e_asin.c, e_acos.c). Differences, all deterministic:
 //  * argument reduction handles |x| <= 2^19 * pi/2 (Cody-Waite, three-part pi/2 with the
-//    cancellation checks of e_rem_pio2.c, without its npio2_hw shortcut table); larger
+//    cancellation checks of e_rem_pio2.c and its npio2_hw shortcut for n < 32); larger
 //    arguments -- never reached on the trace path, whose angles are draws in [0, 2pi),
 //    acos / asin results or texture coordinates -- are reduced by the same three-part
 //    step with n computed the same way (less accurate there, still identical on both sides);
@@ -102,6 +102,11 @@ JF_FN int rem_pio2(double x, double& y0, double& y1) {
     else { z += pio2_2; y0 = z + pio2_2t; y1 = (z - y0) + pio2_2t; }
     return -1;
   }
+  // e_rem_pio2.c's npio2_hw[n-1] is the high word of n * pi/2 (n = 1..32); below n = 32 an argument
+  // whose high word differs from it cannot cancel, and y0 = r - w is taken without the check below.
+  // The high word of fn * (pi/2 rounded) is that table entry for every n < 32 (fn * PIO2 is exactly
+  // (n * pi rounded) / 2; tests/test_jfdlibm.py compares all 31 with the published table), so no
+  // table is indexed here (a dynamically indexed array would live in scratch in the kernels)
   const double t0 = fabs_(x);
   const int32_t n = (int32_t)(t0 * invpio2 + 0.5);
   const double fn = (double)n;
@@ -109,6 +114,7 @@ JF_FN int rem_pio2(double x, double& y0, double& y1) {
   const int32_t j = ix >> 20;
   y0 = r - w;
   int32_t i = j - ((hiw(y0) >> 20) & 0x7ff);
+  if (n < 32 && ix != hiw(fn * JK(1.5707963267948966))) i = 0;  // the quick no-cancellation case
   if (i > 16) {  // 2nd iteration: 118 bits of pi/2
     double t = r;
     w = fn * pio2_2;

@@ -10,6 +10,9 @@
 namespace rt {
 namespace dv {
 #if RT_SPLIT_TU
+// the Perlin tables (c_perm / c_grad3) are per translation unit and only trace.hip uploads its
+// copy: a variant instantiated here must not reach the noise textures
+static_assert((0u & FT_TEX) == 0 && (F_C5 & FT_TEX) == 0, "textured variants belong in trace.hip");
 template __global__ void render_kernel<false, 0u>(SceneD, ParamsD, float*, int32_t*, unsigned long long*);
 template __global__ void render_kernel<false, F_C5>(SceneD, ParamsD, float*, int32_t*, unsigned long long*);
 #endif

@@ -86,6 +86,7 @@ struct rt_scene {
     uint32_t* cost;  // device uint32[ntiles]: probe cost, then one launch's measured wave times
     int ntiles;
     int state;       // 0 probe order; 1 a measuring launch was issued; 2 ordered by measured times
+    void* measured = nullptr;  // hipEvent_t recorded after the measuring launch, on its stream
   };
   std::vector<TileSchedule> schedules;
 };

@@ -339,6 +339,8 @@ void rt_scene_destroy(rt_scene* s) {
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize((hipStream_t)s->stream);
     for (void* p : s->allocs) (void)hipFree(p);
+    for (auto& e : s->schedules)
+      if (e.measured) (void)hipEventDestroy((hipEvent_t)e.measured);
     (void)hipFree(s->outRgb);
     (void)hipFree(s->outArgb);
     if (s->stream) (void)hipStreamDestroy((hipStream_t)s->stream);
@@ -483,6 +485,9 @@ static RenderFn pick_variant(const HostScene& h, uint32_t flags) {
 static int sort_tiles(rt_scene::TileSchedule& e, hipStream_t st) {
   std::vector<uint32_t> cost(e.ntiles);
   hipError_t r = hipStreamSynchronize(st);
+  // the measuring launch may have run on another stream (rt_render's own vs a caller's
+  // rt_render_device stream): wait for it before reading its wave times
+  if (r == hipSuccess && e.measured) r = hipEventSynchronize((hipEvent_t)e.measured);
   if (r == hipSuccess) r = hipMemcpy(cost.data(), e.cost, sizeof(uint32_t) * e.ntiles, hipMemcpyDeviceToHost);
   if (r != hipSuccess) return set_error(RT_E_HIP, std::string("tile schedule: ") + hipGetErrorString(r));
   // sort key: cost in quarter-octave buckets; tiles of one bucket keep row-major order, so
@@ -559,6 +564,17 @@ static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, 
                        (unsigned long long*)nullptr);
   }
   HIPCHK(hipGetLastError());
+  if (P.tcost) {  // a measuring launch: mark its completion for sort_tiles
+    for (auto& e : s->schedules)
+      if (e.cost == P.tcost) {
+        if (!e.measured) {
+          hipEvent_t ev;
+          HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+          e.measured = ev;
+        }
+        HIPCHK(hipEventRecord((hipEvent_t)e.measured, st));
+      }
+  }
   return RT_OK;
 }
 

@@ -245,7 +245,8 @@ int rt_photons_shoot(rt_scene* scene, uint64_t seed, int64_t first, int64_t coun
 int rt_photons_set(rt_scene* scene, const double* pos, const double* pwr, int64_t n);
 
 /* Blocking render into caller-owned HOST buffers (either may be NULL). Runs on the scene's own
-   stream with device output buffers kept across calls (no per-call allocation or device-wide sync).
+   stream with device output buffers kept across calls (no per-call allocation or device-wide sync;
+   they grow to the largest frame rendered and are freed by rt_scene_destroy).
    rgb: float[n_rows*width*3] clamped <=1 per myColor; argb: int32[n_rows*width], reference packing. */
 int rt_render(rt_scene* scene, const rt_render_params* p, float* rgb, int32_t* argb);
 /* Asynchronous render into caller-owned DEVICE buffers on `hip_stream` (hipStream_t, may be NULL).

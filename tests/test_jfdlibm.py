@@ -54,3 +54,19 @@ def test_device_bits_equal_host_bits():
     h = oracle.math_eval(x)
     same = (d.view(np.uint64) == h.view(np.uint64)) | (np.isnan(d) & np.isnan(h))
     assert same.all(), np.argwhere(~same)[:10]
+
+
+# e_rem_pio2.c's npio2_hw (fdlibm 5.3): the high words of n * pi/2, n = 1..32
+NPIO2_HW = [0x3FF921FB, 0x400921FB, 0x4012D97C, 0x401921FB, 0x401F6A7A, 0x4022D97C, 0x4025FDBB, 0x402921FB,
+            0x402C463A, 0x402F6A7A, 0x4031475C, 0x4032D97C, 0x40346B9C, 0x4035FDBB, 0x40378FDB, 0x403921FB,
+            0x403AB41B, 0x403C463A, 0x403DD85A, 0x403F6A7A, 0x40407E4C, 0x4041475C, 0x4042106C, 0x4042D97C,
+            0x4043A28C, 0x40446B9C, 0x404534AC, 0x4045FDBB, 0x4046C6CB, 0x40478FDB, 0x404858EB, 0x404921FB]
+
+
+def test_npio2_hw_is_the_high_word_of_fn_times_pio2():
+    """jfdlibm.h's rem_pio2 takes e_rem_pio2.c's no-cancellation shortcut (n < 32, high word of x
+    != npio2_hw[n-1]) with the table entry computed as hiw(fn * (pi/2 rounded)): equal for every n."""
+    import struct
+    for n in range(1, 33):
+        hi = struct.unpack(">I", struct.pack(">d", float(n) * 1.5707963267948966)[:4])[0]
+        assert hi == NPIO2_HW[n - 1], n
