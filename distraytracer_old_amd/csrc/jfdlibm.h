@@ -114,8 +114,9 @@ JF_FN int rem_pio2(double x, double& y0, double& y1) {
   const int32_t j = ix >> 20;
   y0 = r - w;
   int32_t i = j - ((hiw(y0) >> 20) & 0x7ff);
-  if (n < 32 && ix != hiw(fn * JK(1.5707963267948966))) i = 0;  // the quick no-cancellation case
-  if (i > 16) {  // 2nd iteration: 118 bits of pi/2
+  // 2nd iteration (118 bits of pi/2) unless the quick no-cancellation case applies (tested only
+  // here, where it matters: the common path carries no extra work)
+  if (i > 16 && !(n < 32 && ix != hiw(fn * JK(1.5707963267948966)))) {
     double t = r;
     w = fn * pio2_2;
     r = t - w;

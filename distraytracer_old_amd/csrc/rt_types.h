@@ -57,10 +57,12 @@ struct PrimD {
 struct NodeD {
   double lmin[3], lmax[3];
   int32_t left;
-  int32_t pad[3];   // photon map: left child range (start, count), right child start
+  int32_t pad[3];   // photon map: left child range (start, count), right child start;
+                    // scene BVH: pad[1..2] = the left child's fat-edge bound (double, node_slack)
   double rmin[3], rmax[3];
   int32_t right;
-  int32_t padR[3];  // photon map: right child count, photons in the subtree
+  int32_t padR[3];  // photon map: right child count, photons in the subtree; scene BVH: padR[1..2]
+                    // = the right child's fat-edge bound
 };
 static_assert(sizeof(NodeD) == 128, "NodeD is two 64-B lines");
 struct LeafD {
@@ -79,8 +81,15 @@ struct AccelD {
   int32_t xf;
   int32_t root;      // child ref: >= 0 node, < 0 ~leaf
   int32_t is_list;   // end_list
-  int32_t pad;
+  int32_t flags;     // ACCEL_NEAREST: the nearest-first closest-hit traversal applies (scene_build.cpp)
 };
+// AccelD.flags: a BVH whose leaves are all triangle runs in the accel's own CTM, with a finite
+// fat-edge bound for every node (trace_kernels.h accel_closest_nf)
+enum : int32_t { ACCEL_NEAREST = 1 };
+// A node child's fat-edge bound: every point the reference's triangle test accepts for a
+// triangle below the child lies within this distance of the child's box (per axis; in the
+// accel's object space)
+inline double& node_slack(NodeD& n, int side) { return *reinterpret_cast<double*>(side ? &n.padR[1] : &n.pad[1]); }
 enum : int32_t { TOP_TRI = 0, TOP_PRIM = 1, TOP_ACCEL = 2, TOP_INST = 3 };  // TOP_INST: idx = PT_INST prim
 struct TopD {
   int32_t kind, idx, xf;
@@ -158,6 +167,8 @@ struct SceneD {
   double lensRadius, lensFocal;
   int32_t numRays;  // recursion budget (myScene.numRays = 8)
   int32_t fastSlab; // every BVH box coordinate is 0 or in [2^-200, 2^200] (trace_device.h qdiv)
+  int32_t nearestFirst;  // nearest-first closest-hit traversal where it applies (0: the reference order;
+                         // per launch: RT_RENDER_NOCULL counts the reference algorithm's work)
 };
 
 struct ParamsD {

@@ -603,6 +603,81 @@ void pack_leaves(HostScene& hs) {
   for (AccelD& a : hs.accel) a.root = code(a.root);
 }
 
+// How far outside its edges the reference's triangle test accepts a point (checkInside,
+// myPlanarObject.java:165-175: an edge cross product dotted with the unit normal >= -1e-7, i.e.
+// 1e-7 / |edge| from the edge line): the corners of that enlarged triangle move by at most
+// (d_a + d_b) / sin A. +inf when an angle is too acute to bound (trace.hip tri_world_box, the
+// same bound in world space).
+static double tri_slack(const TriD& T) {
+  double e[3][3], len[3];
+  for (int i = 0; i < 3; ++i) {
+    for (int c = 0; c < 3; ++c) e[i][c] = T.v[(i + 1) % 3][c] - T.v[i][c];
+    len[i] = std::sqrt(e[i][0] * e[i][0] + e[i][1] * e[i][1] + e[i][2] * e[i][2]);
+    if (!(len[i] > 0) || !std::isfinite(len[i])) return INFINITY;
+  }
+  double grow = 0;
+  for (int i = 0; i < 3; ++i) {
+    const int ia = (i + 2) % 3;
+    const double cosA = -(e[ia][0] * e[i][0] + e[ia][1] * e[i][1] + e[ia][2] * e[i][2]) / (len[ia] * len[i]);
+    const double sinA = std::sqrt(std::max(0.0, 1 - cosA * cosA));
+    if (!(sinA > 1e-4)) return INFINITY;
+    const double da = 1e-7 / len[ia] * 1.01 + 1e-12, db = 1e-7 / len[i] * 1.01 + 1e-12;
+    grow = std::max(grow, (da + db) / sinA);
+  }
+  return grow;
+}
+
+// Fat-edge bounds of every node child of the accels that qualify for the nearest-first
+// closest-hit traversal (AccelD.flags): a BVH whose leaves are all triangle runs in the
+// accel's own CTM. A child's bound is its triangles' largest tri_slack plus a relative
+// 2^-30 of its box coordinates (the hit point's own rounding; generous on purpose).
+static void nearest_first_bounds(HostScene& hs) {
+  for (AccelD& a : hs.accel) {
+    a.flags = 0;
+    if (a.is_list || a.root < 0) continue;
+    bool ok = true;
+    std::vector<int32_t> stack{a.root};
+    std::vector<int32_t> order;  // nodes, parents first
+    while (!stack.empty() && ok) {
+      const int32_t r = stack.back();
+      stack.pop_back();
+      order.push_back(r);
+      for (int side = 0; side < 2; ++side) {
+        const int32_t c = side ? hs.node[r].right : hs.node[r].left;
+        if (c >= 0) { stack.push_back(c); continue; }
+        if (!((~c) & LEAF_RUN_FLAG)) { ok = false; break; }  // a LeafD leaf (prims / instances)
+        const int32_t st = ((~c) >> 5) & LEAF_RUN_MAXSTART, cnt = (~c) & 31;
+        for (int i = 0; i < cnt; ++i)
+          if (hs.tri[st + i].xf != a.xf) { ok = false; break; }
+      }
+    }
+    if (!ok) continue;
+    std::vector<double> sub(hs.node.size(), 0.0);  // a node's largest slack over its subtree
+    for (auto it = order.rbegin(); it != order.rend() && ok; ++it) {
+      NodeD& n = hs.node[*it];
+      double m = 0;
+      for (int side = 0; side < 2; ++side) {
+        const int32_t c = side ? n.right : n.left;
+        double s = 0;
+        if (c >= 0) s = sub[c];
+        else {
+          const int32_t st = ((~c) >> 5) & LEAF_RUN_MAXSTART, cnt = (~c) & 31;
+          for (int i = 0; i < cnt; ++i) s = std::max(s, tri_slack(hs.tri[st + i]));
+        }
+        if (!std::isfinite(s)) { ok = false; break; }
+        const double* mn = side ? n.rmin : n.lmin;
+        const double* mx = side ? n.rmax : n.lmax;
+        double mag = 0;
+        for (int k = 0; k < 3; ++k) mag = std::max(mag, std::max(std::fabs(mn[k]), std::fabs(mx[k])));
+        node_slack(n, side) = s * 1.01 + mag * 0x1p-30 + 1e-300;
+        m = std::max(m, s);
+      }
+      sub[*it] = m;
+    }
+    if (ok) a.flags |= ACCEL_NEAREST;
+  }
+}
+
 }  // namespace
 
 int build_host_scene(const rt_scene_desc* d, HostScene& hs) {
@@ -610,6 +685,7 @@ int build_host_scene(const rt_scene_desc* d, HostScene& hs) {
   if (!b.run()) return set_error(RT_E_INVALID, b.err);
   if (hs.leaf.size() >= (size_t)LEAF_RUN_FLAG) return set_error(RT_E_INVALID, "too many BVH leaves");
   pack_leaves(hs);
+  nearest_first_bounds(hs);
   return RT_OK;
 }
 

@@ -554,7 +554,8 @@ static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, 
   int tilesX = ((P.W + P.colStep - 1) / P.colStep + P.tw - 1) / P.tw, tilesY = (P.nrows + P.th - 1) / P.th;
   dim3 grid(dv::xcd_grid(tilesX * tilesY)), block(64);
   SceneD sd = s->dev;
-  if (flags & RT_RENDER_NOCULL) sd.topBound = s->noCullBound;
+  sd.nearestFirst = 1;
+  if (flags & RT_RENDER_NOCULL) { sd.topBound = s->noCullBound; sd.nearestFirst = 0; }
   if (count) {  // counting always runs the all-features kernel
     HIPCHK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long) * RT_ST_N, st));
     hipLaunchKernelGGL((dv::render_kernel<true, dv::FT_ALL>), grid, block, dv::LDS_RENDER_BYTES, st, sd, P, d_rgb, d_argb,

@@ -128,7 +128,7 @@ DEVI AccelD sload_accel(const AccelD* p) {
   AccelD a;
 #pragma unroll
   for (int c = 0; c < 3; ++c) { a.bmin[c] = sload(p->bmin + c); a.bmax[c] = sload(p->bmax + c); }
-  a.xf = sload(&p->xf); a.root = sload(&p->root); a.is_list = sload(&p->is_list); a.pad = 0;
+  a.xf = sload(&p->xf); a.root = sload(&p->root); a.is_list = sload(&p->is_list); a.flags = sload(&p->flags);
   return a;
 }
 DEVI TopD sload_top(const TopD* p) {
@@ -519,6 +519,148 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
   if (local < outer) outer = local;
 }
 
+// ---------------------------------------------------------------------------
+// Nearest-first closest hit (packet), for BVHs of triangle runs in the accel's own CTM
+// (AccelD.flags ACCEL_NEAREST) and rays the in-place re-normalisation no longer changes.
+//
+// The reference visits a BVH left child first and prunes only a RIGHT child, against its left
+// sibling's subtree minimum (accel_closest). Its answer is nevertheless a function of the hits
+// alone: call h* the hit of minimal t over every leaf the reference's box tests reach (Q2 boxes:
+// origin inside = miss), ties to the first in depth-first leaf order -- the triangle index, as
+// pack_leaves numbers triangles in leaf order. If h*'s point lies inside its leaf's box (so the
+// ray enters every box above it before t*), the reference returns h*: it visits every left child
+// whose box is hit, and a right child R above h* is pruned only if the left sibling's subtree
+// holds a hit with t <= entry(R) < t*, which would beat or precede h*. This traversal finds h*
+// with the smallest work: children nearest first, a child skipped when the ray enters its box
+// grown by the fat-edge bound (node_slack: every point the triangle test accepts below it lies
+// within) beyond the best hit so far -- such a subtree holds no hit that could win or tie. The
+// reference's exact box test still decides reachability. A lane whose winner lies outside its
+// leaf box (a fat-edge hit) re-runs the reference traversal (accel_closest_pk). The image is the
+// reference's bit for bit; the counting kernel under RT_RENDER_NOCULL keeps the reference order,
+// so its counters remain the reference algorithm's.
+#ifndef RT_NEAREST_FIRST
+#define RT_NEAREST_FIRST 1
+#endif
+// (not in the photon-map variants: C5's scene has no BVH, and the unused code cost its kernel 10 %
+// through register allocation)
+static constexpr bool NEAREST_FIRST = RT_NEAREST_FIRST != 0;
+DEVI double sload_slack(const NodeD* nd, int side) {
+  return sload(reinterpret_cast<const double*>(side ? &nd->padR[1] : &nd->pad[1]));
+}
+// entry t of the box grown by s on every side (RN products with the reciprocal: within 2^-50 of
+// the exact entry, far inside node_slack's 2^-30 margin); DMAX when the ray misses it
+DEVI double entry_grown(const double* mn, const double* mx, double s, V o, const double* y) {
+  const double t0 = ((mn[0] - s) - o.x) * y[0], t3 = ((mx[0] + s) - o.x) * y[0];
+  const double t1 = ((mn[1] - s) - o.y) * y[1], t4 = ((mx[1] + s) - o.y) * y[1];
+  const double t2 = ((mn[2] - s) - o.z) * y[2], t5 = ((mx[2] + s) - o.z) * y[2];
+  const double lo = fmax(fmax(fmin(t0, t3), fmin(t1, t4)), fmin(t2, t5));
+  const double hi = fmin(fmin(fmax(t0, t3), fmax(t1, t4)), fmax(t2, t5));
+  return (hi >= lo && hi > 0) ? lo : DMAX;
+}
+// a candidate t worth the inside test: it can beat (or, by leaf order, tie) this accel's best
+// and beats the best of the entries before it (their ties win: TreeMap keeps the first)
+struct LimNF {
+  double bt, prev;
+  DEVI bool ok(double t) const { return t <= bt && t < prev; }
+};
+template <bool CNT, uint32_t F>
+DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv ri, WRay& w, const Key& k,
+                           const HitCtx& hc, Best& best, double& outer, Counters& ct) {
+  double bt = DMAX;       // this accel's best hit: t, triangle index (leaf order), point inside its leaf box
+  int32_t bref = INT32_MAX;
+  bool inside = false;
+  uint64_t act = __ballot(1);
+  int sp = 0;
+  int32_t N = uni(A.root);
+  ChildBox cur;           // the box of the child being entered (a leaf's box when N < 0)
+  while (true) {
+    if (N >= 0) {  // internal: both children tested now, the nearer one entered, the other pushed
+      const NodeD* nd = S.node + N;
+      const ChildBox cl = sload_child(nd, 0), cr = sload_child(nd, 1);
+      const double sl = sload_slack(nd, 0), sr = sload_slack(nd, 1);
+      WCNT(C_WNODE, 1);  // a node visit (8(d) prices one at 64 B, as the reference order's)
+      bool hl = false, hr = false;
+      double el = DMAX, er = DMAX;
+      if (in_mask(act)) {
+        if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }
+        const double bnd = fmin(best.t, bt), lim = fmin(bnd + bnd * 0x1p-40, 0x1p1000);  // a miss (DMAX) never passes
+        el = entry_grown(cl.mn, cl.mx, sl, ao, ri.y);
+        er = entry_grown(cr.mn, cr.mx, sr, ao, ri.y);
+        if (el <= lim) hl = box_hit(cl.mn, cl.mx, ao, ad, ri);
+        if (er <= lim) hr = box_hit(cr.mn, cr.mx, ao, ad, ri);
+      }
+      const uint64_t L = __ballot(hl), R = __ballot(hr);
+      if (L && R) {
+        const int fl = (int)__builtin_ctzll(L & R);
+        const bool nearLeft = __builtin_amdgcn_readlane((el <= er) ? 1 : 0, fl) != 0;
+        const uint64_t far = nearLeft ? R : L;
+        pkN()[sp] = (N << 1) | (nearLeft ? 1 : 0);
+        pkM()[sp] = far;
+        if (sp < PK_LDS && in_mask(far)) pkT()[sp * 64 + __lane_id()] = nearLeft ? er : el;
+        sp++;
+        cur = nearLeft ? cl : cr;
+        act = nearLeft ? L : R;
+      } else if (L) {
+        cur = cl; act = L;
+      } else if (R) {
+        cur = cr; act = R;
+      } else {
+        N = INT32_MAX;
+      }
+      if (N != INT32_MAX) { N = cur.ref; continue; }
+    } else {  // a leaf: a run of triangles in leaf order
+      const int32_t c = ~N;
+      const int32_t st = (c >> 5) & LEAF_RUN_MAXSTART, cnt = c & 31;
+      if (CNT && in_mask(act)) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += cnt; }
+      for (int i = 0; i < cnt; ++i) {
+        PKSTAT(P_CT_STEP, act);
+        WCNT(C_WTRI, 1);
+        const TriG T = sload_tri(S.tri + st + i);
+        if (in_mask(act)) {
+          if (CNT) ct.c[C_TRI]++;
+          double t;
+          int args;
+          if (tri_test(T, ao, ad, t, args, LimNF{bt, best.t}) && (t < bt || (t == bt && st + i < bref))) {
+            bt = t;
+            bref = st + i;
+            // the ray enters the leaf box (the reference's slab arithmetic) clearly before t
+            double te;
+            inside = slab_exact(cur.mn, cur.mx, ao, ad, ri, te) && te < t - t * 0x1p-40;
+          }
+        }
+      }
+    }
+    // pop the nearest pending child that some lane still needs
+    N = INT32_MAX;
+    while (sp > 0) {
+      --sp;
+      const int32_t code = uni(pkN()[sp]);
+      uint64_t M = uni64(pkM()[sp]);
+      const ChildBox cb = sload_child(S.node + (code >> 1), code & 1);
+      bool keep = false;
+      if (in_mask(M)) {
+        const double bnd = fmin(best.t, bt), lim = fmin(bnd + bnd * 0x1p-40, 0x1p1000);  // a miss (DMAX) never passes
+        const double e = sp < PK_LDS ? pkT()[sp * 64 + __lane_id()]
+                                     : entry_grown(cb.mn, cb.mx, sload_slack(S.node + (code >> 1), code & 1), ao, ri.y);
+        keep = e <= lim;
+      }
+      M = __ballot(keep);
+      if (M) { cur = cb; act = M; N = cb.ref; break; }
+    }
+    if (N == INT32_MAX) break;
+  }
+  const bool win = bt < best.t;
+  const bool fb = win && !inside;
+  if (__ballot(fb)) {  // fat-edge winners outside their leaf box: the reference traversal decides
+    if (fb) accel_closest_pk<CNT, F>(S, A, ao, ad, ri, w, k, hc, best, outer, ct);
+  }
+  if (win && !fb) {
+    best.t = bt; best.ref = bref; best.top = (int16_t)hc.top; best.inAcc = 1; best.inst = hc.inst;
+    best.ver = w.ver; best.iver = 0;
+    if (bt < outer) outer = bt;
+  }
+}
+
 // myInstance.intersectCheck (mySceneObject.java:119-124): the named object tested with
 // the instance ray (instance CTM inverse x w) as both of its rays; for a named accel
 // that ray is re-normalised in place by its leaves. `local` receives the minimal t.
@@ -623,7 +765,10 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       w.moved = false;
       double local = DMAX;
       PROF_T0(t_acc);
-      if (PK) accel_closest_pk<CNT, F>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
+      if (PK && NEAREST_FIRST && (F & FT_PHOTON) == 0 && S.nearestFirst && (A.flags & ACCEL_NEAREST) &&
+          !__ballot(!(w.stable && ri.fast)))
+        accel_closest_nf<CNT, F>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
+      else if (PK) accel_closest_pk<CNT, F>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
       else accel_closest<CNT, F, false>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
       PROF_ADD(t_acc, R_CLOSEST_ACCEL);
     } else {

@@ -130,10 +130,12 @@ def test_ray_counts_match_oracle(cli, W, spp):
     so = dict(so, implicit=so["sphere"])
     for k in ("camera", "shadow", "refl", "refr", "tri", "quad", "implicit", "light", "texel"):
         assert sg[k] == so[k], (k, sg[k], so[k])
-    # per-wave record loads never exceed the per-lane ones; culling only removes work
+    # per-wave record loads never exceed the per-lane ones; culling only removes top-level work (the
+    # BVHs run nearest-first with culling on, so their node / triangle counts are the kernel's own)
     _, _, sc = g.render_count(W, W, spp=spp, seed=SEED)
     for k in ("node", "tri", "quad", "implicit", "light", "photon"):
         assert sc["w_" + k] <= sc[k], k
+    for k in ("quad", "implicit", "light", "photon"):
         assert sc[k] <= sg[k], k
     for k in ("camera", "shadow", "refl", "refr", "light", "texel"):
         assert sc[k] == sg[k], k

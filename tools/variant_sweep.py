@@ -67,10 +67,8 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "shscan": ["RT_PROF_SH_SCANONLY"],         # shadow rays: the top-level scan only, no tests
     "shnoacc": ["RT_PROF_SH_NOACCEL"],         # shadow rays: no BVH / list entries
     "regions": ["RT_PROF_REGIONS"],           # wave time per region (tools/regions.py)
-    "shc0": ["RT_SHADOW_COMPACT=0"],           # shadow rays traced lane by lane (round-2 loop)
-    "shc1": [],                                # compacted shadow rays (default)
-    "pkstat0": ["RT_PROF_PKSTAT", "RT_SHADOW_COMPACT=0"],
-    "regions0": ["RT_PROF_REGIONS", "RT_SHADOW_COMPACT=0"],
+    "nf0": ["RT_NEAREST_FIRST=0"],             # closest hit in the reference order only (round 2)
+    "nf1": [],                                 # nearest-first closest hit where it applies (default)
 }
 FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS", "g": "RT_MAX_G", "p": "RT_PACKET",
           "l": "RT_PK_LDS", "b": "RT_PH_BATCH", "m": "RT_PK_MASKED"}
