@@ -116,7 +116,10 @@ JF_FN int rem_pio2(double x, double& y0, double& y1) {
   int32_t i = j - ((hiw(y0) >> 20) & 0x7ff);
   // 2nd iteration (118 bits of pi/2) unless the quick no-cancellation case applies (tested only
   // here, where it matters: the common path carries no extra work)
-  if (i > 16 && !(n < 32 && ix != hiw(fn * JK(1.5707963267948966)))) {
+#ifndef RT_JF_NPIO2
+#define RT_JF_NPIO2 1
+#endif
+  if (i > 16 && !(RT_JF_NPIO2 && n < 32 && ix != hiw(fn * JK(1.5707963267948966)))) {
     double t = r;
     w = fn * pio2_2;
     r = t - w;

@@ -166,10 +166,13 @@ struct SceneD {
   int32_t dof;
   double lensRadius, lensFocal;
   int32_t numRays;  // recursion budget (myScene.numRays = 8)
-  int32_t fastSlab; // every BVH box coordinate is 0 or in [2^-200, 2^200] (trace_device.h qdiv)
-  int32_t nearestFirst;  // nearest-first closest-hit traversal where it applies (0: the reference order;
-                         // per launch: RT_RENDER_NOCULL counts the reference algorithm's work)
+  // bit 0 (SCENE_FAST_SLAB): every BVH box coordinate is 0 or in [2^-200, 2^200] (trace_device.h
+  // qdiv); bit 1 (SCENE_NEAREST_FIRST): nearest-first BVH traversals where they apply, set per launch
+  // (RT_RENDER_NOCULL keeps the reference order: its counters are the reference algorithm's work).
+  // One word rather than a new field: the kernels' argument layout stays as it was.
+  int32_t fastSlab;
 };
+enum : int32_t { SCENE_FAST_SLAB = 1, SCENE_NEAREST_FIRST = 2 };
 
 struct ParamsD {
   int32_t W, H, spp, row0, nrows, rowStep;

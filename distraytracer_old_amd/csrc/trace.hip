@@ -247,7 +247,7 @@ static int upload_scene(rt_scene* s) {
   bool ok = true;
   for (const NodeD& n : h.node) ok = ok && in_range(n.lmin, 3) && in_range(n.lmax, 3) && in_range(n.rmin, 3) && in_range(n.rmax, 3);
   for (const AccelD& a : h.accel) ok = ok && in_range(a.bmin, 3) && in_range(a.bmax, 3);
-  d.fastSlab = ok ? 1 : 0;
+  d.fastSlab = ok ? SCENE_FAST_SLAB : 0;
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dv::c_perm), H_PERM, sizeof(H_PERM)));
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dv::c_grad3), H_GRAD3, sizeof(H_GRAD3)));
   void* cnt = nullptr;
@@ -554,8 +554,8 @@ static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, 
   int tilesX = ((P.W + P.colStep - 1) / P.colStep + P.tw - 1) / P.tw, tilesY = (P.nrows + P.th - 1) / P.th;
   dim3 grid(dv::xcd_grid(tilesX * tilesY)), block(64);
   SceneD sd = s->dev;
-  sd.nearestFirst = 1;
-  if (flags & RT_RENDER_NOCULL) { sd.topBound = s->noCullBound; sd.nearestFirst = 0; }
+  sd.fastSlab |= SCENE_NEAREST_FIRST;
+  if (flags & RT_RENDER_NOCULL) { sd.topBound = s->noCullBound; sd.fastSlab &= ~SCENE_NEAREST_FIRST; }
   if (count) {  // counting always runs the all-features kernel
     HIPCHK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long) * RT_ST_N, st));
     hipLaunchKernelGGL((dv::render_kernel<true, dv::FT_ALL>), grid, block, dv::LDS_RENDER_BYTES, st, sd, P, d_rgb, d_argb,

@@ -250,6 +250,21 @@ DEVI bool box_shadow(const double* mn, const double* mx, V o, V d, const RayInv&
   return slab_exact(mn, mx, o, d, ri, te) && (dist - te) > EPS;
 }
 
+// box_shadow that also reports the box's entry t (approximate: the ordering of the nearest-first
+// any-hit traversal, never a decision)
+DEVI bool box_shadow_e(const double* mn, const double* mx, V o, V d, const RayInv& ri, double dist, double& te) {
+  if (ri.fast) {
+    int r = slab_apx(mn, mx, o, ri.y, te);
+    if (r == 0) return false;
+    if (r == 1) {
+      const double g = (dist - te) - EPS, tol = APX * (fabs(te) + fabs(dist));
+      if (g > tol) return true;
+      if (-g > tol) return false;
+    }
+  }
+  return slab_exact(mn, mx, o, d, ri, te) && (dist - te) > EPS;
+}
+
 DEVI int slab_plane(const double* mn, const double* mx, V o, V d) {  // plane idx for myBBox normals
   double ro[3] = {o.x, o.y, o.z}, rd[3] = {d.x, d.y, d.z};
   double biggestMin = -DMAX;

@@ -66,7 +66,8 @@ def lib():
             raise RTError(f"{p} is missing: build it with `python -m distraytracer_old_amd.build`")
         L = ctypes.CDLL(str(p))
         L.rt_last_error.restype = ctypes.c_char_p
-        L.rt_build_id.restype = ctypes.c_char_p
+        if hasattr(L, "rt_build_id"):  # ABI >= 5 (older tuning builds lack it: build_id() -> "unknown")
+            L.rt_build_id.restype = ctypes.c_char_p
         L.rt_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.rt_scene_load_cli.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                         ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(TextureDesc),
@@ -112,7 +113,7 @@ def _name_call(fn, *args) -> str:
 
 def build_id() -> str:
     """The loaded library's build id (rt_build_id: hash of its sources and flags, build.py)."""
-    return lib().rt_build_id().decode()
+    return lib().rt_build_id().decode() if hasattr(lib(), "rt_build_id") else "unknown"
 
 
 def png_name(save_name: str) -> str:

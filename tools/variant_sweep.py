@@ -69,6 +69,11 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "regions": ["RT_PROF_REGIONS"],           # wave time per region (tools/regions.py)
     "nf0": ["RT_NEAREST_FIRST=0"],             # closest hit in the reference order only (round 2)
     "nf1": [],                                 # nearest-first closest hit where it applies (default)
+    "nopio": ["RT_JF_NPIO2=0"],                # rem_pio2 without e_rem_pio2.c's npio2_hw shortcut
+    "an0": ["RT_ANY_NEAR=0"],                  # any-hit BVH traversal left first only
+    "nfan0": ["RT_NEAREST_FIRST=0", "RT_ANY_NEAR=0"],
+    "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
+             "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
 FIELDS = {"w": "RT_RENDER_WAVES", "s": "RT_STACK_LDS", "x": "RT_XCD_CHUNKS", "g": "RT_MAX_G", "p": "RT_PACKET",
           "l": "RT_PK_LDS", "b": "RT_PH_BATCH", "m": "RT_PK_MASKED"}
