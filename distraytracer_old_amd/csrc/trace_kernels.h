@@ -541,8 +541,8 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
 #ifndef RT_NEAREST_FIRST
 #define RT_NEAREST_FIRST 1
 #endif
-// (not in the photon-map variants: C5's scene has no BVH, and the unused code cost its kernel 10 %
-// through register allocation)
+// (not in the photon-map and transparent variants, whose 128-VGPR allocation it perturbs: C5's
+// kernel lost 10 % to the unused code, C4's 3 % -- 583 -> 599 ms -- although its bunnies use it)
 static constexpr bool NEAREST_FIRST = RT_NEAREST_FIRST != 0;
 DEVI double sload_slack(const NodeD* nd, int side) {
   return sload(reinterpret_cast<const double*>(side ? &nd->padR[1] : &nd->pad[1]));
@@ -765,7 +765,8 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       w.moved = false;
       double local = DMAX;
       PROF_T0(t_acc);
-      if (PK && NEAREST_FIRST && (F & FT_PHOTON) == 0 && (S.fastSlab & SCENE_NEAREST_FIRST) && (A.flags & ACCEL_NEAREST) &&
+      if (PK && NEAREST_FIRST && (F & (FT_PHOTON | FT_TRANS)) == 0 && (S.fastSlab & SCENE_NEAREST_FIRST) &&
+          (A.flags & ACCEL_NEAREST) &&
           !__ballot(!(w.stable && ri.fast)))
         accel_closest_nf<CNT, F>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
       else if (PK) accel_closest_pk<CNT, F>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
