@@ -168,11 +168,12 @@ struct SceneD {
   int32_t numRays;  // recursion budget (myScene.numRays = 8)
   // bit 0 (SCENE_FAST_SLAB): every BVH box coordinate is 0 or in [2^-200, 2^200] (trace_device.h
   // qdiv); bit 1 (SCENE_NEAREST_FIRST): nearest-first BVH traversals where they apply, set per launch
-  // (RT_RENDER_NOCULL keeps the reference order: its counters are the reference algorithm's work).
+  // (RT_RENDER_NOCULL keeps the reference order: its counters are the reference algorithm's work);
+  // bit 2 (SCENE_WAVE_CULL): wave-level shadow candidates (shadow_cands), ntop <= 64, culling on.
   // One word rather than a new field: the kernels' argument layout stays as it was.
   int32_t fastSlab;
 };
-enum : int32_t { SCENE_FAST_SLAB = 1, SCENE_NEAREST_FIRST = 2 };
+enum : int32_t { SCENE_FAST_SLAB = 1, SCENE_NEAREST_FIRST = 2, SCENE_WAVE_CULL = 4 };
 
 struct ParamsD {
   int32_t W, H, spp, row0, nrows, rowStep;

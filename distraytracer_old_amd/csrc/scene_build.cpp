@@ -527,6 +527,12 @@ struct Builder {
       ld.radDiff = ld.outerRad - ld.innerRad;
       ld.radius = s.radius;
       std::memcpy(ld.g, s.ctm, sizeof(ld.g));
+      {  // pad[0] = 1: a point / spot light at its object-space origin (identity CTM): every shadow
+         // ray ends there (the device's wave-level shadow cull, trace_kernels.h step_cands)
+        bool ident = true;
+        for (int q = 0; q < 16; ++q) ident = ident && ld.g[q] == ((q % 5 == 0) ? 1.0 : 0.0);
+        ld.pad[0] = (ident && (s.type == RT_LIGHT_POINT || s.type == RT_LIGHT_SPOT)) ? 1 : 0;
+      }
       hs.light.push_back(ld);
     }
     // textures -> Processing pixel ints

@@ -555,7 +555,8 @@ static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, 
   dim3 grid(dv::xcd_grid(tilesX * tilesY)), block(64);
   SceneD sd = s->dev;
   sd.fastSlab |= SCENE_NEAREST_FIRST;
-  if (flags & RT_RENDER_NOCULL) { sd.topBound = s->noCullBound; sd.fastSlab &= ~SCENE_NEAREST_FIRST; }
+  if (sd.ntop <= 64 && !(flags & RT_RENDER_NOWAVECULL)) sd.fastSlab |= SCENE_WAVE_CULL;
+  if (flags & RT_RENDER_NOCULL) { sd.topBound = s->noCullBound; sd.fastSlab &= ~(SCENE_NEAREST_FIRST | SCENE_WAVE_CULL); }
   if (count) {  // counting always runs the all-features kernel
     HIPCHK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long) * RT_ST_N, st));
     hipLaunchKernelGGL((dv::render_kernel<true, dv::FT_ALL>), grid, block, dv::LDS_RENDER_BYTES, st, sd, P, d_rgb, d_argb,

@@ -181,6 +181,9 @@ typedef struct rt_render_params {
    the e-th (hit, light) pair) instead of light by light on the shading lanes: same image (DESIGN.md
    §4 "Compacted shadow rays"; slower on the benchmark configs, so not the default) */
 #define RT_RENDER_SHCOMPACT 8u
+/* turn off the wave-level candidate test of shadow rays against the top-level entries' bounding
+   spheres (DESIGN.md §4 "Wave-level shadow cull"): same image; for A/B timing and testing */
+#define RT_RENDER_NOWAVECULL 16u
 
 typedef struct rt_scene rt_scene;
 

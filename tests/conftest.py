@@ -13,6 +13,12 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "spawns: starts GPU child processes; runs before anything touches the GPU here")
 
 
+def pytest_sessionstart(session):
+    # scenes/bun69k.cli is generated (deterministic, ~1.5 s) and not pushed to the GPU box
+    from distraytracer_old_amd import scenes
+    scenes.ensure_bun69k()
+
+
 def pytest_collection_modifyitems(session, config, items):
     # child processes are started before this process initialises HIP (no exec / fork+exec
     # from a GPU-initialised process): the `spawns` tests go first, in their file order

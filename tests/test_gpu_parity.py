@@ -232,6 +232,23 @@ def test_compacted_shadow_rays_render_identically(cli, W, spp):
         assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32)), flags
 
 
+@pytest.mark.parametrize("cli,W,spp", [("plnts3ColsBunnies.cli", 128, 4), ("p2_t03.cli", 96, 2),
+                                       ("c3spotLight.cli", 96, 2), ("p2_t05.cli", 96, 2), ("c4.cli", 96, 2),
+                                       ("cylinder1.cli", 96, 2)])
+def test_wave_shadow_cull_renders_identically(cli, W, spp):
+    """The wave-level shadow candidate test (SCENE_WAVE_CULL: an entry whose bounding sphere
+    stays farther than the lanes' spread from the wave's first shadow segment is skipped) gives
+    the image of the plain per-lane scan (RT_RENDER_NOWAVECULL) and of the reference's full scan
+    (RT_RENDER_NOCULL) bit for bit: spot / point / disk lights, moving spheres, cylinders, glass."""
+    scenes.ensure_bun69k()
+    g = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+    ra, aa = g.render(W, W, spp=spp, seed=SEED)
+    for flags in (rt.RENDER_NOWAVECULL, rt.RENDER_NOCULL):
+        rb, ab = g.render(W, W, spp=spp, seed=SEED, flags=flags)
+        assert np.array_equal(aa, ab), flags
+        assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32)), flags
+
+
 def test_photon_shards_merge_to_the_full_prepass(tmp_path):
     """Multi-GPU photon pre-pass (8(e)): shards shot separately and merged in rank order give
     the single-GPU photon_list bit for bit, and the same image."""

@@ -70,7 +70,9 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "nf0": ["RT_NEAREST_FIRST=0"],             # closest hit in the reference order only (round 2)
     "nf1": [],                                 # nearest-first closest hit where it applies (default)
     "nopio": ["RT_JF_NPIO2=0"],                # rem_pio2 without e_rem_pio2.c's npio2_hw shortcut
-    "an0": ["RT_ANY_NEAR=0"],                  # any-hit BVH traversal left first only
+    "an0": ["RT_ANY_NEAR=0"],
+    "wc0": ["RT_WAVE_CULL=0"],                 # no wave-level shadow candidates (the r03l kernel)
+    "wc1": [],                                 # wave-level shadow candidates per shading step (default)
     "nfan0": ["RT_NEAREST_FIRST=0", "RT_ANY_NEAR=0"],
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
