@@ -721,6 +721,89 @@ DEVI bool top_culled(const SceneD& S, int i, const WRay& w, double lim) {
   return a > 0 && a * a > h2 * (1 + 1e-12) + 1e-12 * (oc2 + R2);
 }
 
+// ---------------------------------------------------------------------------
+// Wave-level shadow candidates (SCENE_WAVE_CULL, round 3). calcShadow (myScene.java:879-885)
+// tests every objList entry; the per-lane cull (top_culled) skips an entry whose bounding sphere
+// the lane's ray misses, but pays that sphere test for every entry, lane and shadow ray -- C4's
+// 21 entries x 6 lights made the shadow scan ~40 % of its wave time. For a point / spot light
+// whose CTM is the identity (LightD.pad[0] = 1, set by the host), lane l's shadow ray runs along
+// nrmz(origin - p_l) for |p_l - origin| (calcShadowColor :98-121), so a blocking hit
+// (0 < t < dist - 1e-7, Q7) lies on the segment [p_l, origin]; every such segment lies within sp
+// of [p_f, origin], f the wave's first shading lane and sp the spread of the hit points (max-norm
+// x sqrt 3: the point at fraction s of lane l's segment is within |p_l - p_f| of the point at
+// fraction s of f's). An entry whose bounding sphere (radius R, trace.hip top_bounds) stays
+// farther than R + sp from [p_f, origin] therefore holds no blocker for any lane of the wave.
+// Once per shading step (light_sum), the shading lanes test the (light, entry) pairs round robin
+// -- one pass for C4's 6 x 21 -- and OR each light's candidate bits into LDS (the compacted-shadow
+// group area, idle in this path); shadowed_ then jumps from candidate to candidate. The test is a
+// superset of the capsule (line distance <= Q and projection within [-Q, |v| + Q]) with slack far
+// above its rounding; unbounded entries (quads, planes, top-level triangles, instances), disk or
+// transformed lights and lights past the 8th keep every entry. A skipped entry's in-place
+// re-normalisation of the ray (myRay.java:93) is still applied, in order, before the next test,
+// so every test sees the reference's direction: images are bit-identical (GPU tests), only the
+// entries visited change. Measured: C4 582 -> 501 ms (the per-light form 561 ms; as a real call
+// 711-792 ms: it is inlined; the same test for the closest-hit scan of a step's rays, 521 ms:
+// dropped; profiles/r03n_*, r03o_*).
+#ifndef RT_WAVE_CULL
+#define RT_WAVE_CULL 1
+#endif
+// variants with the wave-level shadow cull: non-triangle primitives, no photon map (C4's); the
+// host enables it per launch (SCENE_WAVE_CULL: ntop <= 64, culling on)
+template <uint32_t F>
+static constexpr bool WAVE_CULL = RT_WAVE_CULL && (F & FT_PRIM) != 0 && (F & FT_PHOTON) == 0;
+DEVI double rdl(double v, int L) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, L), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), L);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+DEVI lds_u64* wcM() { return (lds_u64*)(pkB() + LDS_BYTES + SUM_BYTES); }
+// the candidate bits of lights 0..7 for the hit points p of the active lanes (wave-scope LDS
+// atomics of the active lanes only: the ockl wave reductions assume no holes in the exec mask)
+DEVI void step_cands(const SceneD& S, V p) {
+  lds_u64* M = wcM();
+  const uint64_t act = __ballot(1);
+  const int f = (int)__builtin_ctzll(act);
+  const V pf = mk(rdl(p.x, f), rdl(p.y, f), rdl(p.z, f));
+  // the spread: sp >= 0 (or NaN), so its bits order as its value; a NaN makes every entry a candidate
+  double sp = fmax(fmax(fabs(p.x - pf.x), fabs(p.y - pf.y)), fabs(p.z - pf.z));
+  M[0] = 0;
+  __hip_atomic_fetch_max(M, __builtin_bit_cast(uint64_t, sp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  sp = __builtin_bit_cast(double, __hip_atomic_load(M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)) * 1.7320508075688776;
+  const int nl = S.nlight < GRP_MAX ? S.nlight : GRP_MAX, nt = S.ntop, np = nl * nt;
+  for (int q = 0; q < nl; ++q) M[q] = 0;
+  const int nact = __popcll(act);
+  const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  const uint32_t rcp = (1u << 20) / (uint32_t)nt + 1;  // q / nt exactly for q < 512, nt <= 64
+  const double pn = fmax(fmax(fabs(pf.x), fabs(pf.y)), fabs(pf.z));
+  for (int q0 = 0; q0 < np; q0 += nact) {
+    const int q = q0 + rank;
+    if (q < np) {
+      const int li = (int)(((uint32_t)q * rcp) >> 20), i = q - li * nt;
+      const LightD& L = S.light[li];
+      const double* b = S.topBound + 4 * i;
+      const double R = b[3];
+      bool cand = true;
+      if (L.pad[0] == 1 && R > 0) {
+        const V v = mk(L.origin[0] - pf.x, L.origin[1] - pf.y, L.origin[2] - pf.z);
+        const double vv = v.x * v.x + v.y * v.y + v.z * v.z, vl = sqrt(vv);
+        const V w = mk(b[0] - pf.x, b[1] - pf.y, b[2] - pf.z);
+        const double wv = w.x * v.x + w.y * v.y + w.z * v.z, ww = w.x * w.x + w.y * w.y + w.z * w.z;
+        const double Q = (R + sp + 1e-9 * (1 + vl + sp + pn + R)) * (1 + 1e-9), Q2 = Q * Q;
+        const double perp = ww * vv - wv * wv, slackP = 1e-9 * (ww * vv + Q2 * vv);
+        const double slackT = 1e-9 * (sqrt(ww) * vl + vv), qv = Q * vl;
+        // "far" from comparisons that are false on NaN: a NaN / Inf segment stays a candidate
+        cand = !(perp > Q2 * vv + slackP || wv < -qv - slackT || wv > vv + qv + slackT);
+      }
+      if (cand) __hip_atomic_fetch_or(M + li, 1ull << i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+  }
+}
+DEVI void step_cands_all() {
+  for (int q = 0; q < GRP_MAX; ++q) wcM()[q] = ~0ull;
+}
+// light li's candidate bits, read where the scan starts (no register holds them before it)
+DEVI uint64_t step_cand(int li) { return li < GRP_MAX ? uni64(*(volatile lds_u64*)(wcM() + li)) : ~0ull; }
+
 // findClosestRayHit (myScene.java:888-903): objList scan, TreeMap keeps the first of equal t
 #ifndef RT_PACKET
 #define RT_PACKET 1
@@ -939,88 +1022,6 @@ DEVI bool inst_any(const SceneD& S, int32_t ii, const WRay& w, const Key& k, dou
   }
   return false;
 }
-// ---------------------------------------------------------------------------
-// Wave-level shadow candidates (SCENE_WAVE_CULL, round 3). calcShadow (myScene.java:879-885)
-// tests every objList entry; the per-lane cull (top_culled) skips an entry whose bounding sphere
-// the lane's ray misses, but pays that sphere test for every entry, lane and shadow ray -- C4's
-// 21 entries x 6 lights made the shadow scan ~40 % of its wave time. For a point / spot light
-// whose CTM is the identity (LightD.pad[0] = 1, set by the host), lane l's shadow ray runs along
-// nrmz(origin - p_l) for |p_l - origin| (calcShadowColor :98-121), so a blocking hit
-// (0 < t < dist - 1e-7, Q7) lies on the segment [p_l, origin]; every such segment lies within sp
-// of [p_f, origin], f the wave's first shading lane and sp the spread of the hit points (max-norm
-// x sqrt 3: the point at fraction s of lane l's segment is within |p_l - p_f| of the point at
-// fraction s of f's). An entry whose bounding sphere (radius R, trace.hip top_bounds) stays
-// farther than R + sp from [p_f, origin] therefore holds no blocker for any lane of the wave.
-// Once per shading step (light_sum), the shading lanes test the (light, entry) pairs round robin
-// -- one pass for C4's 6 x 21 -- and OR each light's candidate bits into LDS (the compacted-shadow
-// group area, idle in this path); shadowed_ then jumps from candidate to candidate. The test is a
-// superset of the capsule (line distance <= Q and projection within [-Q, |v| + Q]) with slack far
-// above its rounding; unbounded entries (quads, planes, top-level triangles, instances), disk or
-// transformed lights and lights past the 8th keep every entry. A skipped entry's in-place
-// re-normalisation of the ray (myRay.java:93) is still applied, in order, before the next test,
-// so every test sees the reference's direction: images are bit-identical (GPU tests), only the
-// entries visited change. Measured: C4 582 -> 501 ms (the per-light form 561 ms; as a real call
-// 711-792 ms: it is inlined; profiles/r03n_*).
-#ifndef RT_WAVE_CULL
-#define RT_WAVE_CULL 1
-#endif
-// variants with the wave-level shadow cull: non-triangle primitives, no photon map (C4's); the
-// host enables it per launch (SCENE_WAVE_CULL: ntop <= 64, culling on)
-template <uint32_t F>
-static constexpr bool WAVE_CULL = RT_WAVE_CULL && (F & FT_PRIM) != 0 && (F & FT_PHOTON) == 0;
-DEVI double rdl(double v, int L) {
-  const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, L), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), L);
-  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-DEVI lds_u64* wcM() { return (lds_u64*)(pkB() + LDS_BYTES + SUM_BYTES); }
-// the candidate bits of lights 0..7 for the hit points p of the active lanes (wave-scope LDS
-// atomics of the active lanes only: the ockl wave reductions assume no holes in the exec mask)
-DEVI void step_cands(const SceneD& S, V p) {
-  lds_u64* M = wcM();
-  const uint64_t act = __ballot(1);
-  const int f = (int)__builtin_ctzll(act);
-  const V pf = mk(rdl(p.x, f), rdl(p.y, f), rdl(p.z, f));
-  // the spread: sp >= 0 (or NaN), so its bits order as its value; a NaN makes every entry a candidate
-  double sp = fmax(fmax(fabs(p.x - pf.x), fabs(p.y - pf.y)), fabs(p.z - pf.z));
-  M[0] = 0;
-  __hip_atomic_fetch_max(M, __builtin_bit_cast(uint64_t, sp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-  sp = __builtin_bit_cast(double, __hip_atomic_load(M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)) * 1.7320508075688776;
-  const int nl = S.nlight < GRP_MAX ? S.nlight : GRP_MAX, nt = S.ntop, np = nl * nt;
-  for (int q = 0; q < nl; ++q) M[q] = 0;
-  const int nact = __popcll(act);
-  const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-  const uint32_t rcp = (1u << 20) / (uint32_t)nt + 1;  // q / nt exactly for q < 512, nt <= 64
-  const double pn = fmax(fmax(fabs(pf.x), fabs(pf.y)), fabs(pf.z));
-  for (int q0 = 0; q0 < np; q0 += nact) {
-    const int q = q0 + rank;
-    if (q < np) {
-      const int li = (int)(((uint32_t)q * rcp) >> 20), i = q - li * nt;
-      const LightD& L = S.light[li];
-      const double* b = S.topBound + 4 * i;
-      const double R = b[3];
-      bool cand = true;
-      if (L.pad[0] == 1 && R > 0) {
-        const V v = mk(L.origin[0] - pf.x, L.origin[1] - pf.y, L.origin[2] - pf.z);
-        const double vv = v.x * v.x + v.y * v.y + v.z * v.z, vl = sqrt(vv);
-        const V w = mk(b[0] - pf.x, b[1] - pf.y, b[2] - pf.z);
-        const double wv = w.x * v.x + w.y * v.y + w.z * v.z, ww = w.x * w.x + w.y * w.y + w.z * w.z;
-        const double Q = (R + sp + 1e-9 * (1 + vl + sp + pn + R)) * (1 + 1e-9), Q2 = Q * Q;
-        const double perp = ww * vv - wv * wv, slackP = 1e-9 * (ww * vv + Q2 * vv);
-        const double slackT = 1e-9 * (sqrt(ww) * vl + vv), qv = Q * vl;
-        // "far" from comparisons that are false on NaN: a NaN / Inf segment stays a candidate
-        cand = !(perp > Q2 * vv + slackP || wv < -qv - slackT || wv > vv + qv + slackT);
-      }
-      if (cand) __hip_atomic_fetch_or(M + li, 1ull << i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    }
-  }
-}
-DEVI void step_cands_all() {
-  for (int q = 0; q < GRP_MAX; ++q) wcM()[q] = ~0ull;
-}
-// light li's candidate bits, read where the scan starts (no register holds them before it)
-DEVI uint64_t step_cand(int li) { return li < GRP_MAX ? uni64(*(volatile lds_u64*)(wcM() + li)) : ~0ull; }
-
 // myScene.calcShadow (myScene.java:879-885). WC: light li's wave-level candidates only
 // (step_cands / step_cands_all have written them)
 template <bool CNT, uint32_t F, bool PK = false, bool WC = false>
