@@ -200,6 +200,36 @@ static std::vector<double> top_bounds(const HostScene& h) {
   return b;
 }
 
+// World planes of the top-level quads / planes (after the 4 * ntop sphere bounds, 8 doubles per
+// entry: orientation A's and B's plane as unit normal + offset, zero normal = none). A hit of
+// orientation A lies on N_A . x + d_A = 0 in object space (trace_device.h planar_test), so on
+// n . y + d = 0 in world space with n = A^-T N_A, d = d_A - n . b (y = A x + b, the entry's CTM).
+// The wave-level shadow cull (trace_kernels.h step_cands) skips the entry for a wave whose shadow
+// segments all stay strictly on one side of both planes.
+static std::vector<double> top_planes(const HostScene& h) {
+  std::vector<double> b(8 * h.top.size(), 0.0);
+  for (size_t i = 0; i < h.top.size(); ++i) {
+    const TopD& t = h.top[i];
+    if (t.kind != TOP_PRIM) continue;
+    const PrimD& P = h.prim[t.idx];
+    if (P.type != PT_QUAD && P.type != PT_PLANE) continue;
+    const double* g = h.xf[t.xf].g;
+    const double* inv = h.xf[t.xf].inv;
+    for (int o = 0; o < 2; ++o) {
+      const double* N = P.a + (o ? 15 : 12);
+      const double D = P.a[o ? 19 : 18];
+      double n[3];
+      for (int c = 0; c < 3; ++c) n[c] = inv[0 * 4 + c] * N[0] + inv[1 * 4 + c] * N[1] + inv[2 * 4 + c] * N[2];
+      const double d = D - (n[0] * g[3] + n[1] * g[7] + n[2] * g[11]);
+      const double len = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+      if (!(len > 0) || !std::isfinite(len) || !std::isfinite(d)) { std::fill(&b[8 * i], &b[8 * i] + 8, 0.0); break; }
+      for (int c = 0; c < 3; ++c) b[8 * i + 4 * o + c] = n[c] / len;
+      b[8 * i + 4 * o + 3] = d / len;
+    }
+  }
+  return b;
+}
+
 static int upload_scene(rt_scene* s) {
   HostScene& h = s->hs;
   SceneD& d = s->dev;
@@ -217,7 +247,10 @@ static int upload_scene(rt_scene* s) {
   }
   d.ntop = (int)h.top.size();
   {
-    const std::vector<double> tb = top_bounds(h), none(tb.size(), -1.0);
+    std::vector<double> tb = top_bounds(h), none(tb.size(), -1.0);
+    const std::vector<double> tp = top_planes(h);
+    tb.insert(tb.end(), tp.begin(), tp.end());
+    none.insert(none.end(), tp.size(), 0.0);
     if ((rc = upload(s, tb, &d.topBound)) || (rc = upload(s, none, &s->noCullBound))) return rc;
   }
   d.nlight = (int)h.light.size();

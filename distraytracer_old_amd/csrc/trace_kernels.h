@@ -541,6 +541,12 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
 #ifndef RT_NEAREST_FIRST
 #define RT_NEAREST_FIRST 1
 #endif
+#ifndef RT_NF_TRANS  // nearest-first closest hit in the transparent (non-photon) variants too
+#define RT_NF_TRANS 0
+#endif
+#ifndef RT_AN_TRANS  // nearest-first any-hit order in the transparent variants too
+#define RT_AN_TRANS 0
+#endif
 // (not in the photon-map and transparent variants, whose 128-VGPR allocation it perturbs: C5's
 // kernel lost 10 % to the unused code, C4's 3 % -- 583 -> 599 ms -- although its bunnies use it)
 static constexpr bool NEAREST_FIRST = RT_NEAREST_FIRST != 0;
@@ -783,7 +789,20 @@ DEVI void step_cands(const SceneD& S, V p) {
       const double* b = S.topBound + 4 * i;
       const double R = b[3];
       bool cand = true;
-      if (L.pad[0] == 1 && R > 0) {
+      if (L.pad[0] == 1 && !(R > 0)) {  // a quad / plane: the segments strictly on one side of its plane(s)
+        const double* pl = S.topBound + 4 * nt + 8 * i;
+        const double m = 1e-6 * (1 + pn + fmax(fmax(fabs(L.origin[0]), fabs(L.origin[1])), fabs(L.origin[2])));
+        bool off = pl[0] != 0 || pl[1] != 0 || pl[2] != 0;
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+          const double* q = pl + 4 * o;
+          const double sP = q[0] * pf.x + q[1] * pf.y + q[2] * pf.z + q[3];
+          const double sL = q[0] * L.origin[0] + q[1] * L.origin[1] + q[2] * L.origin[2] + q[3];
+          const double mm = m * (1 + fabs(q[3]));
+          off = off && ((sP - sp > mm && sL > mm) || (sP + sp < -mm && sL < -mm));
+        }
+        cand = !off;
+      } else if (L.pad[0] == 1) {
         const V v = mk(L.origin[0] - pf.x, L.origin[1] - pf.y, L.origin[2] - pf.z);
         const double vv = v.x * v.x + v.y * v.y + v.z * v.z, vl = sqrt(vv);
         const V w = mk(b[0] - pf.x, b[1] - pf.y, b[2] - pf.z);
@@ -848,7 +867,7 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       w.moved = false;
       double local = DMAX;
       PROF_T0(t_acc);
-      if (PK && NEAREST_FIRST && (F & (FT_PHOTON | FT_TRANS)) == 0 && (S.fastSlab & SCENE_NEAREST_FIRST) &&
+      if (PK && NEAREST_FIRST && (F & (FT_PHOTON | (RT_NF_TRANS ? 0 : FT_TRANS))) == 0 && (S.fastSlab & SCENE_NEAREST_FIRST) &&
           (A.flags & ACCEL_NEAREST) &&
           !__ballot(!(w.stable && ri.fast)))
         accel_closest_nf<CNT, F>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
@@ -946,7 +965,7 @@ template <bool CNT, uint32_t F>
 DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
   const RayInv ri = ray_inv(ao, ad, S.fastSlab & SCENE_FAST_SLAB);
   // (C3's triangles-only variant gains 2 %; the transparent variants lose as much: not there)
-  const bool nearf = RT_ANY_NEAR && (F & FT_TRANS) == 0 && (S.fastSlab & SCENE_NEAREST_FIRST) && !__ballot(!w.stable);
+  const bool nearf = RT_ANY_NEAR && (RT_AN_TRANS || (F & FT_TRANS) == 0) && (S.fastSlab & SCENE_NEAREST_FIRST) && !__ballot(!w.stable);
   PkStack st;
   int sp = 0;
   uint64_t act = __ballot(1);

@@ -73,6 +73,11 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "an0": ["RT_ANY_NEAR=0"],
     "wc0": ["RT_WAVE_CULL=0"],                 # no wave-level shadow candidates (the r03l kernel)
     "wc1": [],                                 # wave-level shadow candidates per shading step (default)
+    "base": [],                                # the default build
+    "wp1": [],                                 # the default build (+ quad / plane sides in the wave cull)
+    "nft": ["RT_NF_TRANS=1"],                  # nearest-first closest hit in C4's transparent variant
+    "ant": ["RT_AN_TRANS=1"],                  # nearest-first any-hit order there
+    "nftant": ["RT_NF_TRANS=1", "RT_AN_TRANS=1"],
     "nfan0": ["RT_NEAREST_FIRST=0", "RT_ANY_NEAR=0"],
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
