@@ -200,7 +200,7 @@ static std::vector<double> top_bounds(const HostScene& h) {
   return b;
 }
 
-// World planes of the top-level quads / planes (after the 4 * ntop sphere bounds, 8 doubles per
+// World planes of the top-level quads / planes / triangles (after the 4 * ntop sphere bounds, 8 doubles per
 // entry: orientation A's and B's plane as unit normal + offset, zero normal = none). A hit of
 // orientation A lies on N_A . x + d_A = 0 in object space (trace_device.h planar_test), so on
 // n . y + d = 0 in world space with n = A^-T N_A, d = d_A - n . b (y = A x + b, the entry's CTM).
@@ -210,14 +210,23 @@ static std::vector<double> top_planes(const HostScene& h) {
   std::vector<double> b(8 * h.top.size(), 0.0);
   for (size_t i = 0; i < h.top.size(); ++i) {
     const TopD& t = h.top[i];
-    if (t.kind != TOP_PRIM) continue;
-    const PrimD& P = h.prim[t.idx];
-    if (P.type != PT_QUAD && P.type != PT_PLANE) continue;
+    double NA[3], NB[3], DA, DB;
+    if (t.kind == TOP_PRIM && (h.prim[t.idx].type == PT_QUAD || h.prim[t.idx].type == PT_PLANE)) {
+      const PrimD& P = h.prim[t.idx];
+      for (int c = 0; c < 3; ++c) { NA[c] = P.a[12 + c]; NB[c] = P.a[15 + c]; }
+      DA = P.a[18]; DB = P.a[19];
+    } else if (t.kind == TOP_TRI) {  // tri_test: orientation B is -n with dB
+      const TriD& T = h.tri[t.idx];
+      for (int c = 0; c < 3; ++c) { NA[c] = T.n[c]; NB[c] = -T.n[c]; }
+      DA = T.dA; DB = T.dB;
+    } else {
+      continue;
+    }
     const double* g = h.xf[t.xf].g;
     const double* inv = h.xf[t.xf].inv;
     for (int o = 0; o < 2; ++o) {
-      const double* N = P.a + (o ? 15 : 12);
-      const double D = P.a[o ? 19 : 18];
+      const double* N = o ? NB : NA;
+      const double D = o ? DB : DA;
       double n[3];
       for (int c = 0; c < 3; ++c) n[c] = inv[0 * 4 + c] * N[0] + inv[1 * 4 + c] * N[1] + inv[2 * 4 + c] * N[2];
       const double d = D - (n[0] * g[3] + n[1] * g[7] + n[2] * g[11]);

@@ -755,8 +755,11 @@ DEVI bool top_culled(const SceneD& S, int i, const WRay& w, double lim) {
 #endif
 // variants with the wave-level shadow cull: non-triangle primitives, no photon map (C4's); the
 // host enables it per launch (SCENE_WAVE_CULL: ntop <= 64, culling on)
+#ifndef RT_WC_TRI  // also in the triangles-only variants (C3's: two ground triangles and a BVH)
+#define RT_WC_TRI 0
+#endif
 template <uint32_t F>
-static constexpr bool WAVE_CULL = RT_WAVE_CULL && (F & FT_PRIM) != 0 && (F & FT_PHOTON) == 0;
+static constexpr bool WAVE_CULL = RT_WAVE_CULL && ((F & FT_PRIM) != 0 || RT_WC_TRI) && (F & FT_PHOTON) == 0;
 DEVI double rdl(double v, int L) {
   const uint64_t b = __builtin_bit_cast(uint64_t, v);
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, L), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), L);

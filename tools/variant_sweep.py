@@ -75,6 +75,7 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "wc1": [],                                 # wave-level shadow candidates per shading step (default)
     "base": [],                                # the default build
     "wp1": [],                                 # the default build (+ quad / plane sides in the wave cull)
+    "wtri": ["RT_WC_TRI=1"],                   # the wave cull in the triangles-only variant (C3) too
     "nft": ["RT_NF_TRANS=1"],                  # nearest-first closest hit in C4's transparent variant
     "ant": ["RT_AN_TRANS=1"],                  # nearest-first any-hit order there
     "nftant": ["RT_NF_TRANS=1", "RT_AN_TRANS=1"],
