@@ -249,6 +249,62 @@ def test_wave_shadow_cull_renders_identically(cli, W, spp):
         assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32)), flags
 
 
+WAVE_CULL_SCENE = """fov 60
+background 0.2 0.2 0.3
+point_light 2 5 0 .6 .6 .6
+spotlight -2 6 -2  0.3 -1 -0.2  15 40  .5 .5 .5
+push
+translate 0.5 1 -3
+point_light 0 1 0 .3 .3 .3
+pop
+push
+translate 0 -1 -4
+rotate 20 0 1 0
+rotate 10 1 0 0
+scale 3 1 2
+diffuse .7 .7 .7 .1 .1 .1
+begin quad
+vertex -1 0 -1
+vertex 1 0 -1
+vertex 1 0 1
+vertex -1 0 1
+end
+pop
+push
+translate 0 0 -6
+rotate 30 0 1 0
+diffuse .3 .6 .3 .1 .1 .1
+begin quad
+vertex -2 -1 0
+vertex 2 -1 0
+vertex 2 2 0
+vertex -2 2 0
+end
+pop
+diffuse .8 .2 .2 .1 .1 .1
+sphere .5 -0.8 -0.3 -3.5
+push
+scale 1 1.5 1
+sphere .4 0.9 0.0 -3
+pop
+cyl .3 1  1.5 -1 -4.5
+"""
+
+
+def test_wave_shadow_cull_transformed_quads(tmp_path):
+    """The wave-level cull's world planes (A^-T N, d - n.b of each quad's CTM) and bounding
+    spheres under rotated / scaled CTMs, a light under a translation (not eligible when its CTM
+    applies), point and spot lights: bit-identical to the per-lane scan and to the full scan."""
+    (tmp_path / "wc.cli").write_text(WAVE_CULL_SCENE)
+    g = rt.Scene.load_cli("wc.cli", scene_dir=tmp_path, textures={})
+    ra, aa = g.render(96, 96, spp=4, seed=SEED)
+    assert len(np.unique(aa)) > 50  # lit, shadowed and background pixels
+    for flags in (rt.RENDER_NOWAVECULL, rt.RENDER_NOCULL):
+        rb, ab = g.render(96, 96, spp=4, seed=SEED, flags=flags)
+        assert np.array_equal(aa, ab), flags
+        assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32)), flags
+
+
 def test_photon_shards_merge_to_the_full_prepass(tmp_path):
     """Multi-GPU photon pre-pass (8(e)): shards shot separately and merged in rank order give
     the single-GPU photon_list bit for bit, and the same image."""
