@@ -743,13 +743,15 @@ DEVI bool top_culled(const SceneD& S, int i, const WRay& w, double lim) {
 // -- one pass for C4's 6 x 21 -- and OR each light's candidate bits into LDS (the compacted-shadow
 // group area, idle in this path); shadowed_ then jumps from candidate to candidate. The test is a
 // superset of the capsule (line distance <= Q and projection within [-Q, |v| + Q]) with slack far
-// above its rounding; unbounded entries (quads, planes, top-level triangles, instances), disk or
-// transformed lights and lights past the 8th keep every entry. A skipped entry's in-place
+// above its rounding. Quads, planes and top-level triangles (no bounding sphere) are skipped when
+// the wave's segments stay strictly on one side of their world plane(s) (trace.hip top_planes,
+// after the spheres in topBound); instances, disk or transformed lights and lights past the 8th
+// keep every entry. A skipped entry's in-place
 // re-normalisation of the ray (myRay.java:93) is still applied, in order, before the next test,
 // so every test sees the reference's direction: images are bit-identical (GPU tests), only the
-// entries visited change. Measured: C4 582 -> 501 ms (the per-light form 561 ms; as a real call
-// 711-792 ms: it is inlined; the same test for the closest-hit scan of a step's rays, 521 ms:
-// dropped; profiles/r03n_*, r03o_*).
+// entries visited change. Measured: C4 582 -> 501 ms with the spheres, 472 ms with the plane
+// sides (the per-light form 561 ms; as a real call 711-792 ms: it is inlined; the same test for
+// the closest-hit scan of a step's rays, 521 ms: dropped; profiles/r03n_*, r03o_*, r03r_*).
 #ifndef RT_WAVE_CULL
 #define RT_WAVE_CULL 1
 #endif
