@@ -10,16 +10,19 @@ from distraytracer_old_amd import multigpu, rt, scenes  # noqa: E402
 
 BANDS = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [multigpu.BAND]
 ORDERS = ((0, "schedule"), (rt.RENDER_ROWMAJOR, "row-major")) if len(sys.argv) <= 1 else ((0, "schedule"),)
+CFG = sys.argv[2] if len(sys.argv) > 2 else "C3"  # tools/band_timing.py 8 C4
+cli, W, H, spp, seed = scenes.CONFIGS[CFG]
 scenes.ensure_bun69k()
-s = rt.Scene.load_cli("c3_bun69k.cli", textures=scenes.prepare("c3_bun69k.cli"))
+s = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+s.build_photons(seed)
 for flags, name in ORDERS:
-    full = s.time_render(1024, 1024, spp=16, seed=0x5EED0001, iters=5, flags=flags)
-    print(name, "full %.3f ms" % full)
+    full = s.time_render(W, H, spp=spp, seed=seed, iters=5, flags=flags)
+    print(CFG, name, "full %.3f ms" % full)
     for band, world in [(b, w) for b in BANDS for w in (2, 4, 8)]:
         ts = []
         for rank in range(world):
-            r0, r1, step, b = multigpu.rows_of(rank, world, 1024, band)
-            ts.append(s.time_render(1024, 1024, spp=16, seed=0x5EED0001, rows=(r0, r1), row_step=step, row_band=b,
+            r0, r1, step, b = multigpu.rows_of(rank, world, H, band)
+            ts.append(s.time_render(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=step, row_band=b,
                                     iters=5, flags=flags))
         print(" ", "band", band, "N", world, "max %.3f mean %.3f ideal %.3f eff %.3f" % (max(ts), sum(ts) / len(ts), full / world,
                                                                        full / world / max(ts)))
