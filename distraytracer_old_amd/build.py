@@ -85,18 +85,23 @@ def build(force: bool = False, verbose: bool = False, defines: list[str] | None 
     bid = build_id(defines)
     target.parent.mkdir(parents=True, exist_ok=True)
     tmp = target.with_suffix(".so.tmp%d" % os.getpid())
-    objs, logs = [], []
     tag = "" if out is None else target.stem + "."
-    for src in SOURCES:  # .hip -> device+host; .cpp -> host-only C++ (no device pass)
+    objs, procs = [], []
+    for src in SOURCES:  # .hip -> device+host; .cpp -> host-only C++ (no device pass); compiled in parallel
         obj = target.parent / (tag + src + ".o")
         lang = [] if src.endswith(".hip") else ["-x", "c++"]
         cmd = [HIPCC, *COMPILE_FLAGS, *SOURCE_FLAGS.get(src, []), *_extra_flags(src, defines), f'-DRT_BUILD_ID="{bid}"',
                *lang, "-c", str(CSRC / src), "-o", str(obj)]
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        logs.append(r.stderr)
-        if r.returncode != 0:
-            raise RuntimeError(f"hipcc failed on {src}:\n" + r.stderr[-4000:])
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)))
         objs.append(str(obj))
+    logs, failed = [], None
+    for src, pr in procs:
+        err = pr.communicate()[1]
+        logs.append(err)
+        if pr.returncode != 0 and failed is None:
+            failed = f"hipcc failed on {src}:\n" + err[-4000:]
+    if failed:
+        raise RuntimeError(failed)
     r = subprocess.run([HIPCC, "-shared", "--offload-arch=gfx950", "-o", str(tmp), *objs], capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n" + r.stderr[-4000:])

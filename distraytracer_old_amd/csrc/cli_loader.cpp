@@ -5,8 +5,11 @@
 // stack). It emits the flattened rt_scene_desc that a JNI myScene subclass
 // would hand over, then calls rt_scene_create().
 //
-// Commands outside the hot-path scope are rejected with RT_E_PARSE.
+// Unknown commands are reported on stderr and skipped, as readRTFile's default case does
+// (myRTFileReader.java:343-345); malformed arguments of known commands fail with RT_E_PARSE.
 #include <cctype>
+#include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <map>
 #include <sstream>
@@ -57,6 +60,7 @@ static bool named_color(std::string n, Clr& c) {
 
 struct CliLoader {
   std::string dir, saveName;
+  int ignored = 0;  // unknown commands skipped (myRTFileReader.java:343-345)
   int refine = -1;  // `refine on|off` (myScene.setRefine, myRTFileReader.java:111); -1 = not given
   std::map<std::string, int> texIndex;
   std::vector<Mat> stack{Mat::ident()};
@@ -301,7 +305,9 @@ struct CliLoader {
     rt_prim_desc poly;
     bool inPoly = false;
     int vc = 0;
+    int lineNo = -1;
     while (std::getline(f, line)) {
+      ++lineNo;
       std::vector<std::string> t;
       {  // PApplet.splitTokens(line, " ")
         std::string cur;
@@ -563,9 +569,10 @@ struct CliLoader {
           refine = v == "on" ? 1 : 0;
         } else if (c == "reset_timer" || c == "print_timer") {
           // timers are outside the kernel path
-        } else {
-          err = "unsupported command '" + c + "' in " + fname;
-          return false;
+        } else {  // readRTFile's default case (myRTFileReader.java:343-345): report and go on
+          std::fprintf(stderr, "When reading %s unknown command encountered : '%s' on line : [%d] : %s\n", fname.c_str(),
+                       c.c_str(), lineNo, line.c_str());
+          ++ignored;
         }
       } catch (const std::exception& e) {
         err = "parse error in " + fname + " at '" + c + "': " + e.what();

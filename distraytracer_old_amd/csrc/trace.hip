@@ -404,8 +404,8 @@ static int make_params(rt_scene* s, const rt_render_params* p, ParamsD& P) {
   if (P.spp <= 0) return set_error(RT_E_INVALID, "rays_per_pixel is 0 (scene has no fov/rays_per_pixel; Q26)");
   // the compacted shadow rays hand a shading lane's RNG key to another lane packed in 64 bits
   // (dv::key_pack): pixel index < 2^32, sample < 2^20
-  if ((int64_t)P.W * P.H > (int64_t)UINT32_MAX || P.spp >= (1 << 20))
-    return set_error(RT_E_INVALID, "image larger than 2^32 pixels or spp >= 2^20");
+  if ((p->flags & RT_RENDER_SHCOMPACT) && ((int64_t)P.W * P.H > (int64_t)UINT32_MAX || P.spp >= (1 << 20)))
+    return set_error(RT_E_INVALID, "RT_RENDER_SHCOMPACT: image larger than 2^32 pixels or spp >= 2^20");
   const int band = p->row_band <= 1 ? 1 : p->row_band;
   P.row0 = p->row0;
   P.rowStep = step;

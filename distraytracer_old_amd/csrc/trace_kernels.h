@@ -1052,7 +1052,10 @@ template <bool CNT, uint32_t F, bool PK = false, bool WC = false>
 DEVI bool shadowed_(const SceneD& S, WRay& w, const Key& k, double dist, Counters& ct, int li) {
   const uint64_t cand = WC ? step_cand(li) : ~0ull;
   for (int i = 0; i < S.ntop; ++i) {
-    if (WC) {  // on to the next candidate; the skipped entries' in-place re-normalisations still apply
+    // on to the next candidate; the skipped entries' in-place re-normalisations still apply. The
+    // candidate word covers entries 0..63 (SCENE_WAVE_CULL needs ntop <= 64; otherwise it is ~0):
+    // past it every entry is tested (a shift by >= 64 would wrap on the device and loop forever)
+    if (WC && i < 64) {
       const uint64_t rest = cand & (~0ull << i);
       const int nx = rest ? (int)__builtin_ctzll(rest) : S.ntop;
       for (int j = i; j < nx && !w.stable; ++j) renorm(w);

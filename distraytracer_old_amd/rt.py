@@ -250,6 +250,13 @@ class Scene:
         _check(lib().rt_render(self._h, ctypes.byref(p), rgb.ctypes.data, argb.ctypes.data), "rt_render")
         return rgb, argb
 
+    def render_argb_into(self, argb, W, H, spp=0, seed=0x5EED0001, flags=0):
+        """The JNI draw() call: rt_render of the whole frame into a caller-owned
+        host ARGB buffer (rndrdImg.pixels), no float plane; blocks until the pixels are there."""
+        p = params(W, H, spp, seed, None, 1, flags, 1)
+        assert argb.shape == (H, W) and argb.dtype == np.int32 and argb.flags.c_contiguous
+        _check(lib().rt_render(self._h, ctypes.byref(p), None, argb.ctypes.data), "rt_render")
+
     def refine_steps(self, W, H) -> list[int]:
         """The `refine on` pass steps of a W x H render (myScene.setRefine); [1] without refine."""
         buf = np.zeros(16, dtype=np.int32)

@@ -179,7 +179,9 @@ typedef struct rt_render_params {
 #define RT_RENDER_NOCULL 4u
 /* trace the shadow rays of a wave's shading step compacted (ballot + prefix count: lane e traces
    the e-th (hit, light) pair) instead of light by light on the shading lanes: same image (DESIGN.md
-   §4 "Compacted shadow rays"; slower on the benchmark configs, so not the default) */
+   §4 "Compacted shadow rays"; slower on the benchmark configs, so not the default). It packs a
+   lane's RNG key into 64 bits, so it needs width * height <= 2^32 and spp < 2^20 (RT_E_INVALID
+   otherwise); renders without the flag have no such limit */
 #define RT_RENDER_SHCOMPACT 8u
 /* turn off the wave-level candidate test of shadow rays against the top-level entries' bounding
    spheres (DESIGN.md §4 "Wave-level shadow cull"): same image; for A/B timing and testing */

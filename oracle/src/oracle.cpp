@@ -1646,6 +1646,7 @@ struct Loader {
   std::map<std::string, GeomBase*> named;  // namedObjs (myScene.java:378-387)
   int curNumRaysPerPxl = 0;
   std::string err;
+  int ignored = 0;  // unknown commands skipped (myRTFileReader.java:343-345)
 
   std::shared_ptr<CTM> cur_ctm() { return std::make_shared<CTM>(build_ctm(stack.back())); }
   void set_surface(Color d, Color a, Color sp, double ph, double kr) {
@@ -2206,9 +2207,8 @@ struct Loader {
         } else if (c == "reset_timer" || c == "print_timer" || c == "refine") {
           // timers and the progressive `refine` preview are ignored (documented override)
         } else {
-          // remaining commands are outside the hot-path scope
-          err = "unsupported command: " + c;
-          return false;
+          // myRTFileReader.java:343-345: the default case prints the line and reading goes on
+          ++ignored;
         }
       } catch (const std::exception& e) {
         err = "parse error in " + fname + " at command '" + c + "': " + e.what();

@@ -130,12 +130,12 @@ def test_ray_counts_match_oracle(cli, W, spp):
     so = dict(so, implicit=so["sphere"])
     for k in ("camera", "shadow", "refl", "refr", "tri", "quad", "implicit", "light", "texel"):
         assert sg[k] == so[k], (k, sg[k], so[k])
-    # per-wave record loads never exceed the per-lane ones; culling only removes top-level work (the
-    # BVHs run nearest-first with culling on, so their node / triangle counts are the kernel's own)
+    # per-wave record loads never exceed the per-lane ones; culling only removes work (the counting
+    # kernel is the all-features variant: reference child order in every BVH)
     _, _, sc = g.render_count(W, W, spp=spp, seed=SEED)
     for k in ("node", "tri", "quad", "implicit", "light", "photon"):
         assert sc["w_" + k] <= sc[k], k
-    for k in ("quad", "implicit", "light", "photon"):
+    for k in ("node", "tri", "quad", "implicit", "light", "photon"):
         assert sc[k] <= sg[k], k
     for k in ("camera", "shadow", "refl", "refr", "light", "texel"):
         assert sc[k] == sg[k], k
@@ -213,6 +213,22 @@ def test_specialised_kernel_equals_generic(cli, W, spp):
     rg, ag = g.render(W, W, spp=spp, seed=SEED, flags=rt.RENDER_GENERIC)
     assert np.array_equal(as_, ag)
     assert np.array_equal(rs.view(np.uint32), rg.view(np.uint32))
+
+
+@pytest.mark.parametrize("cli,W,spp", [("plnts3ColsBunnies.cli", 96, 2), ("t11.cli", 64, 1), ("p2_t05.cli", 64, 2)])
+def test_compacted_shadow_rays_oracle_parity(cli, W, spp):
+    """RT_RENDER_SHCOMPACT against the oracle (not only against the default HIP path): C4's scene,
+    the photon-map Cornell box and the disk light, in the scene's variant."""
+    scenes.ensure_bun69k()
+    tex = scenes.prepare(cli)
+    g = rt.Scene.load_cli(cli, textures=tex)
+    o = OracleScene(scenes.SCENE_DIR, cli, tex)
+    if cli == "t11.cli":  # the same photon_list on both sides (test_c5_full_prepass_and_k200_gather_parity)
+        g.build_photons(SEED)
+        o.build_photons(SEED)
+    rg, ag = g.render(W, W, spp=spp, seed=SEED, flags=rt.RENDER_SHCOMPACT)
+    ro, ao, _ = o.render(W, W, spp=spp, seed=SEED)
+    assert_exact_decisions(compare(rg, ag, ro, ao))
 
 
 @pytest.mark.parametrize("cli,W,spp", [("c3_bun69k.cli", 128, 4), ("plnts3ColsBunnies.cli", 96, 4),
@@ -303,6 +319,49 @@ def test_wave_shadow_cull_transformed_quads(tmp_path):
         rb, ab = g.render(96, 96, spp=4, seed=SEED, flags=flags)
         assert np.array_equal(aa, ab), flags
         assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32)), flags
+
+
+@pytest.mark.parametrize("cli", ["c2torus.cli", "old_t07a.cli", "rect_test.cli", "p4_t06Alt.cli", "c4InSphere.cli"])
+def test_ignored_command_scenes_parity(cli):
+    """Scenes with commands readRTFile does not know (`torus`, `backgroun`, `color` / `rect`,
+    `marble2`: reported and skipped, myRTFileReader.java:343-345) and c4InSphere (moonmap4k.jpg,
+    11 point lights: lights past the wave-level cull's 8) render as the oracle does."""
+    g, o, (rg, ag), (ro, ao) = both(cli, 96, 96, 1)
+    assert_exact_decisions(compare(rg, ag, ro, ao))
+
+
+def _many_entries_scene(n_side):
+    """n_side^2 spheres (alternately diffuse and mirror) over a ground quad, point + spot lights:
+    more than 64 objList entries when n_side >= 9."""
+    lines = ["fov 60", "background 0.1 0.1 0.2", "point_light 3 6 2 .6 .6 .6",
+             "spotlight -3 7 -4  0.3 -1 -0.2  20 45  .5 .5 .5", "diffuse .6 .6 .6 .1 .1 .1",
+             "begin quad", "vertex -30 -1 -60", "vertex 30 -1 -60", "vertex 30 -1 10", "vertex -30 -1 10", "end"]
+    for i in range(n_side):
+        for j in range(n_side):
+            if (i + j) % 2:
+                lines.append(f"shiny .2 .2 .6 .05 .05 .1 .5 .5 .5 20 0.4")
+            else:
+                lines.append(f"diffuse .8 .{i % 9 + 1} .{j % 9 + 1} .1 .1 .1")
+            lines.append(f"sphere 0.35 {-3.2 + 0.8 * j:.2f} {-0.6 + 0.1 * i:.2f} {-4.5 - 0.9 * i:.2f}")
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.parametrize("n_side", [8, 9])
+def test_more_than_64_top_level_entries(tmp_path, n_side):
+    """objList with 65 (8x8 spheres + a quad) and 82 entries: past the wave-level shadow cull's
+    64-entry candidate word every entry is scanned (no shift past 63, no endless loop). The
+    default render equals the per-lane scan, the reference's full scan and the oracle."""
+    (tmp_path / "many.cli").write_text(_many_entries_scene(n_side))
+    g = rt.Scene.load_cli("many.cli", scene_dir=tmp_path, textures={})
+    assert g.info()["objects"] == n_side * n_side + 1
+    ra, aa = g.render(64, 64, spp=2, seed=SEED)
+    for flags in (rt.RENDER_NOWAVECULL, rt.RENDER_NOCULL, rt.RENDER_GENERIC):
+        rb, ab = g.render(64, 64, spp=2, seed=SEED, flags=flags)
+        assert np.array_equal(aa, ab), flags
+        assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32)), flags
+    o = OracleScene(tmp_path, "many.cli")
+    ro, ao, _ = o.render(64, 64, spp=2, seed=SEED)
+    assert_exact_decisions(compare(ra, aa, ro, ao))
 
 
 def test_photon_shards_merge_to_the_full_prepass(tmp_path):
