@@ -5,9 +5,10 @@ metric  "Mray/s + achieved HBM GB/s, bun69k.cli 1024^2 16spp, 1/2/4/8 GPU"
 workload C3 = scenes/c3_bun69k.cli (data/p3_t09.cli without `wood`) with the
          synthetic bun69k (69,451 triangles), 1024x1024, 16 spp, seed 0x5EED0001.
 
-One step = one full C3 frame: every rank renders its rows (rank r renders the
-8-row bands r, r+N, r+2N, ... -- interleaved for load balance) with the HIP kernel into a
-device buffer, then (N>1) the per-rank ARGB tiles are gathered to rank 0
+One step = one full C3 frame: every rank renders its part with the HIP kernel into a device
+buffer -- N > 1: the frame's wave tiles dealt to ranks by their measured wave times
+(multigpu.balanced_tiles; --partition bands: 8-row bands r, r+N, ...) -- then (N>1) the per-rank
+ARGB pixels are gathered to rank 0
 over RCCL (`dist.gather`: one point-to-point send per rank over xGMI) and
 re-interleaved there (the ARGB ints the reference's rndrdImg.pixels holds); frame i's exchange
 overlaps frame i+1's render
@@ -219,6 +220,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--partition", default="tiles", choices=["tiles", "bands"],
+                    help="N > 1: cost-balanced wave tiles (default) or interleaved 8-row bands")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N-rank step on fewer GPUs (tiles staged to host; ranks share devices)")
     args = ap.parse_args()
@@ -272,15 +275,20 @@ def main():
         torch.cuda.synchronize()
         photon_s = time.perf_counter() - t
     # the exchanged frame is the reference's output, ARGB ints (rndrdImg.pixels): 4 bytes a pixel
-    rr = multigpu.RankRenderer(scene, W, H, spp, seed, dist, stage_host=(args.backend == "gloo"), planes=("argb",))
+    rr = multigpu.RankRenderer(scene, W, H, spp, seed, dist, stage_host=(args.backend == "gloo"), planes=("argb",),
+                               partition=args.partition)
     r0, r1, rstep, band = rr.rows
 
     # exact per-frame counters (instrumented runs, outside the timed region): the kernel as it
     # runs (top-level culling on: the record loads it issues) and the reference algorithm's work
     # (RT_RENDER_NOCULL: every objList entry tested for every ray, SURVEY 8(d)'s per-ray bytes)
-    _, _, st = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=rstep, row_band=band)
-    _, _, sr = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=rstep, row_band=band,
-                                  flags=rt.RENDER_NOCULL)
+    if rr.partition == "tiles":
+        st = scene.render_tiles_count(rr.p, rr.tiles)
+        sr = scene.render_tiles_count(rt.params(W, H, spp=spp, seed=seed, flags=rt.RENDER_NOCULL), rr.tiles)
+    else:
+        _, _, st = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=rstep, row_band=band)
+        _, _, sr = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=rstep, row_band=band,
+                                      flags=rt.RENDER_NOCULL)
     counts = torch.tensor([traced_rays(st), algorithmic_bytes(sr), st["camera"], wave_bytes(st), algorithmic_bytes(st)],
                           dtype=torch.float64, device=coll_dev)
     if dist:
@@ -374,8 +382,10 @@ def main():
                     f"scene scenes/{cli} (SURVEY 8(d) {args.config}); synthetic inputs where the reference's are missing",
             "config": {"workload": workload, "width": W, "height": H, "spp": spp, "seed": seed,
                        "rays_per_frame": int(rays_frame), "camera_samples": int(cam_frame),
-                       "parallelism": f"{multigpu.BAND}-row bands interleaved over {world} rank(s)" +
-                                      (f" + {args.backend} gather of the ARGB tiles to rank 0" if world > 1 else "")},
+                       "parallelism": ("1 GPU" if world == 1 else
+                                       (f"cost-balanced wave tiles over {world} ranks" if rr.partition == "tiles" else
+                                        f"{multigpu.BAND}-row bands interleaved over {world} ranks") +
+                                       f" + {args.backend} gather of the ARGB pixels to rank 0")},
             "camera_msamples_per_s": cam_frame / (ms_per_step / 1e3) / 1e6,
             "kernel_ms_max_over_ranks": kern_ms_max,
             "host_path_ms_per_step": host_ms,

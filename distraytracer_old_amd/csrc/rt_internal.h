@@ -77,6 +77,8 @@ struct rt_scene {
   float* outRgb = nullptr;
   int32_t* outArgb = nullptr;
   size_t outCap = 0;  // pixels
+  void* stage = nullptr;  // pinned host staging of rt_render's read-back (hipHostMalloc, grow-only)
+  size_t stageCap = 0;    // bytes
   void* stream = nullptr;  // hipStream_t
   const double* noCullBound = nullptr;  // device [ntop][4] of -1 (RT_RENDER_NOCULL)
   // tile schedules (longest tiles first) per tile layout (trace.hip `schedule`)
@@ -89,4 +91,9 @@ struct rt_scene {
     void* measured = nullptr;  // hipEvent_t recorded after the measuring launch, on its stream
   };
   std::vector<TileSchedule> schedules;
+  struct TileList {  // rt_render_tiles_device: a validated tile list and its device copy
+    std::vector<int32_t> host;
+    int32_t* dev = nullptr;
+  };
+  std::vector<TileList> tileLists;
 };

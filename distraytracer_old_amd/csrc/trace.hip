@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <mutex>
 #include <string>
 
@@ -377,7 +378,7 @@ int rt_scene_photons(const rt_scene* s, double* pos, double* pwr, int64_t n, int
 
 void rt_scene_destroy(rt_scene* s) {
   if (!s) return;
-  if (!s->allocs.empty() || s->stream || s->outRgb || s->outArgb) {
+  if (!s->allocs.empty() || s->stream || s->outRgb || s->outArgb || !s->tileLists.empty() || s->stage) {
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize((hipStream_t)s->stream);
     for (void* p : s->allocs) (void)hipFree(p);
@@ -385,6 +386,8 @@ void rt_scene_destroy(rt_scene* s) {
       if (e.measured) (void)hipEventDestroy((hipEvent_t)e.measured);
     (void)hipFree(s->outRgb);
     (void)hipFree(s->outArgb);
+    for (auto& t : s->tileLists) (void)hipFree(t.dev);
+    if (s->stage) (void)hipHostFree(s->stage);
     if (s->stream) (void)hipStreamDestroy((hipStream_t)s->stream);
   }
   delete s;
@@ -584,17 +587,23 @@ static int schedule(rt_scene* s, ParamsD& P, bool count, hipStream_t st) {
   return RT_OK;
 }
 
+// tiles: an explicit tile list (rt_render_tiles_device) -- ntiles blocks, block b renders tiles[b]
 static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, int32_t* d_argb, bool count,
-                  hipStream_t st) {
+                  hipStream_t st, const int32_t* tiles = nullptr, int ntiles = 0) {
   ParamsD P = P0;
+  int tilesX = ((P.W + P.colStep - 1) / P.colStep + P.tw - 1) / P.tw, tilesY = (P.nrows + P.th - 1) / P.th;
+  dim3 grid(dv::xcd_grid(tilesX * tilesY)), block(64);
+  if (tiles) {
+    P.order = const_cast<int32_t*>(tiles);
+    P.tcost = nullptr;
+    grid = dim3(ntiles);
+  }
 #ifndef RT_NO_SCHEDULE
-  if (!(flags & RT_RENDER_ROWMAJOR)) {
+  else if (!(flags & RT_RENDER_ROWMAJOR)) {
     int rc = schedule(s, P, count, st);
     if (rc) return rc;
   }
 #endif
-  int tilesX = ((P.W + P.colStep - 1) / P.colStep + P.tw - 1) / P.tw, tilesY = (P.nrows + P.th - 1) / P.th;
-  dim3 grid(dv::xcd_grid(tilesX * tilesY)), block(64);
   SceneD sd = s->dev;
   sd.fastSlab |= SCENE_NEAREST_FIRST;
   if (sd.ntop <= 64 && !(flags & RT_RENDER_NOWAVECULL)) sd.fastSlab |= SCENE_WAVE_CULL;
@@ -643,15 +652,29 @@ static int render_host(rt_scene* s, const rt_render_params* p, float* rgb, int32
     HIPCHK(hipMalloc(&s->outArgb, npx * sizeof(int32_t)));
     s->outCap = npx;
   }
+  // the read-back goes through pinned staging (a DMA at link speed; a copy into pageable memory is
+  // staged by the runtime in small pieces), then one host memcpy into the caller's buffers
+  const size_t nb = (rgb ? npx * 3 * sizeof(float) : 0) + (argb ? npx * sizeof(int32_t) : 0);
+  if (nb > s->stageCap) {
+    HIPCHK(hipStreamSynchronize(st));
+    (void)hipHostFree(s->stage);
+    s->stage = nullptr; s->stageCap = 0;
+    HIPCHK(hipHostMalloc(&s->stage, nb, hipHostMallocDefault));
+    s->stageCap = nb;
+  }
+  char* stg = (char*)s->stage;
+  const size_t nrgb = rgb ? npx * 3 * sizeof(float) : 0;
   rc = launch(s, P, p->flags, s->outRgb, s->outArgb, stats != nullptr, st);
   hipError_t e = hipSuccess;
-  if (rc == RT_OK && rgb) e = hipMemcpyAsync(rgb, s->outRgb, npx * 3 * sizeof(float), hipMemcpyDeviceToHost, st);
-  if (rc == RT_OK && e == hipSuccess && argb) e = hipMemcpyAsync(argb, s->outArgb, npx * sizeof(int32_t), hipMemcpyDeviceToHost, st);
+  if (rc == RT_OK && rgb) e = hipMemcpyAsync(stg, s->outRgb, nrgb, hipMemcpyDeviceToHost, st);
+  if (rc == RT_OK && e == hipSuccess && argb) e = hipMemcpyAsync(stg + nrgb, s->outArgb, npx * sizeof(int32_t), hipMemcpyDeviceToHost, st);
   if (rc == RT_OK && e == hipSuccess && stats)
     e = hipMemcpyAsync(stats, s->counters, sizeof(uint64_t) * RT_ST_N, hipMemcpyDeviceToHost, st);
   hipError_t se = hipStreamSynchronize(st);  // the call blocks until the frame is in the caller's buffers
   if (rc == RT_OK && e != hipSuccess) rc = set_error(RT_E_HIP, hipGetErrorString(e));
   if (rc == RT_OK && se != hipSuccess) rc = set_error(RT_E_HIP, std::string("render kernel: ") + hipGetErrorString(se));
+  if (rc == RT_OK && rgb) std::memcpy(rgb, stg, nrgb);
+  if (rc == RT_OK && argb) std::memcpy(argb, stg + nrgb, npx * sizeof(int32_t));
   return rc;
 }
 
@@ -704,6 +727,131 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, float* d_rgb, int32
   if (rc) return rc;
   HIPCHK(hipSetDevice(s->device));
   return launch(s, P, p->flags, d_rgb, d_argb, false, (hipStream_t)stream);
+}
+
+static void tile_layout(const ParamsD& P, int32_t out[4]) {
+  const int ncols = (P.W + P.colStep - 1) / P.colStep, tilesX = (ncols + P.tw - 1) / P.tw;
+  out[0] = tilesX * ((P.nrows + P.th - 1) / P.th);
+  out[1] = tilesX;
+  out[2] = P.tw;
+  out[3] = P.th;
+}
+
+int rt_tile_layout(rt_scene* s, const rt_render_params* p, int32_t* out) {
+  if (!out) return set_error(RT_E_INVALID, "rt_tile_layout: null out");
+  ParamsD P;
+  int rc = make_params(s, p, P);
+  if (rc) return rc;
+  tile_layout(P, out);
+  return RT_OK;
+}
+
+int rt_tile_costs(rt_scene* s, const rt_render_params* p, uint32_t* cost, int cap) {
+  if (!cost || cap < 0) return set_error(RT_E_INVALID, "rt_tile_costs: bad buffer");
+  if (p && (p->flags & RT_RENDER_ROWMAJOR)) return set_error(RT_E_INVALID, "rt_tile_costs: RT_RENDER_ROWMAJOR has no costs");
+  ParamsD P;
+  int rc = make_params(s, p, P);
+  if (rc) return rc;
+  int32_t lay[4];
+  tile_layout(P, lay);
+  if (P.nrows * (int64_t)((P.W + P.colStep - 1) / P.colStep) < (1 << 16)) {  // not scheduled: unit costs
+    for (int i = 0; i < lay[0] && i < cap; ++i) cost[i] = 1;
+    return lay[0];
+  }
+  // plain renders of the layout until one has measured its waves (schedule(): state >= 1)
+  for (int it = 0; it < 3; ++it) {
+    rt_scene::TileSchedule* e = nullptr;
+    char key[160];
+    std::snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%.17g", P.W, P.H, P.row0, P.nrows, P.rowStep, P.band,
+                  P.colStep, P.tw, P.th, P.G, P.viewZ);
+    for (auto& x : s->schedules)
+      if (x.key == key) { e = &x; break; }
+    if (e && e->state >= 1) {
+      HIPCHK(hipSetDevice(s->device));
+      if (s->stream) HIPCHK(hipStreamSynchronize((hipStream_t)s->stream));
+      if (e->measured) HIPCHK(hipEventSynchronize((hipEvent_t)e->measured));
+      std::vector<uint32_t> c(e->ntiles);
+      HIPCHK(hipMemcpy(c.data(), e->cost, sizeof(uint32_t) * e->ntiles, hipMemcpyDeviceToHost));
+      for (int i = 0; i < e->ntiles && i < cap; ++i) cost[i] = c[i];
+      return e->ntiles;
+    }
+    rt_render_params q = *p;
+    q.flags &= ~(uint32_t)RT_RENDER_ROWMAJOR;
+    rc = render_host(s, &q, nullptr, nullptr, nullptr);
+    if (rc) return rc;
+  }
+  return set_error(RT_E_INVALID, "rt_tile_costs: the layout was not measured");
+}
+
+// the device copy of a validated tile list (rt_render_tiles_device / rt_render_tiles_count)
+static int tile_list(rt_scene* s, const ParamsD& P, const int32_t* tiles, int ntiles, const int32_t** dev) {
+  if (!tiles || ntiles <= 0) return set_error(RT_E_INVALID, "tile list: empty");
+  if (dv::XCD_CHUNKS != 0) return set_error(RT_E_INVALID, "tile list: built with RT_XCD_CHUNKS");
+  int32_t lay[4];
+  tile_layout(P, lay);
+  if (ntiles > lay[0]) return set_error(RT_E_INVALID, "tile list: more tiles than the layout has");
+  rt_scene::TileList* L = nullptr;
+  for (auto& x : s->tileLists)
+    if (x.host.size() == (size_t)ntiles && std::memcmp(x.host.data(), tiles, sizeof(int32_t) * ntiles) == 0) { L = &x; break; }
+  if (!L) {
+    for (int i = 0; i < ntiles; ++i)
+      if (tiles[i] < 0 || tiles[i] >= lay[0]) return set_error(RT_E_INVALID, "tile list: tile index out of range");
+    if (s->tileLists.size() >= 16) {  // oldest out (its launches may be on streams we do not know: drain the device)
+      HIPCHK(hipDeviceSynchronize());
+      (void)hipFree(s->tileLists.front().dev);
+      s->tileLists.erase(s->tileLists.begin());
+    }
+    rt_scene::TileList t;
+    t.host.assign(tiles, tiles + ntiles);
+    HIPCHK(hipMalloc(&t.dev, sizeof(int32_t) * ntiles));
+    HIPCHK(hipMemcpy(t.dev, tiles, sizeof(int32_t) * ntiles, hipMemcpyHostToDevice));
+    s->tileLists.push_back(std::move(t));
+    L = &s->tileLists.back();
+  }
+  *dev = L->dev;
+  return RT_OK;
+}
+
+int rt_render_tiles_count(rt_scene* s, const rt_render_params* p, const int32_t* tiles, int ntiles, uint64_t* stats) {
+  if (!stats) return set_error(RT_E_INVALID, "null stats");
+  ParamsD P;
+  int rc = make_params(s, p, P);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(s->device));
+  const int32_t* dt = nullptr;
+  rc = tile_list(s, P, tiles, ntiles, &dt);
+  if (rc) return rc;
+  if (!s->stream) {
+    hipStream_t st;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    s->stream = st;
+  }
+  hipStream_t st = (hipStream_t)s->stream;
+  const size_t npx = (size_t)P.nrows * P.W;
+  float* d_rgb = nullptr;
+  int32_t* d_argb = nullptr;
+  HIPCHK(hipMalloc(&d_rgb, npx * 3 * sizeof(float)));
+  hipError_t e = hipMalloc(&d_argb, npx * sizeof(int32_t));
+  if (e == hipSuccess) rc = launch(s, P, p->flags, d_rgb, d_argb, true, st, dt, ntiles);
+  if (e == hipSuccess && rc == RT_OK) e = hipMemcpyAsync(stats, s->counters, sizeof(uint64_t) * RT_ST_N, hipMemcpyDeviceToHost, st);
+  hipError_t se = hipStreamSynchronize(st);
+  (void)hipFree(d_rgb);
+  (void)hipFree(d_argb);
+  if (rc == RT_OK && e != hipSuccess) rc = set_error(RT_E_HIP, hipGetErrorString(e));
+  if (rc == RT_OK && se != hipSuccess) rc = set_error(RT_E_HIP, std::string("count kernel: ") + hipGetErrorString(se));
+  return rc;
+}
+
+int rt_render_tiles_device(rt_scene* s, const rt_render_params* p, const int32_t* tiles, int ntiles, float* d_rgb,
+                           int32_t* d_argb, void* stream) {
+  ParamsD P;
+  int rc = make_params(s, p, P);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(s->device));
+  const int32_t* dt = nullptr;
+  rc = tile_list(s, P, tiles, ntiles, &dt);
+  if (rc) return rc;
+  return launch(s, P, p->flags, d_rgb, d_argb, false, (hipStream_t)stream, dt, ntiles);
 }
 
 int rt_time_render(rt_scene* s, const rt_render_params* p, int warmup, int iters, double* avg_ms) {

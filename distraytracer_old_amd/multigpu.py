@@ -7,6 +7,12 @@ Every rank's tile is padded to the same row count (a multiple of the band) so on
 `gather` (RCCL point-to-point over xGMI; gloo in CPU tests) brings all float-RGB
 tiles to rank 0, and `assemble` re-interleaves them.
 
+Cost-balanced tiles (the default of bench.py's N-GPU step): the frame's wave tiles are dealt
+to ranks from their measured wave times (`balanced_tiles`: rank 0 calibrates the whole frame,
+rt_tile_costs, and broadcasts the costs, so every rank derives the same partition); each rank
+renders its tile list into a whole-frame device buffer (rt_render_tiles_device), packs its pixels
+into a compact tile buffer (`tile_pixels` order) for the gather, and rank 0 scatters them back.
+
 Pixels, their RNG keys and their per-pixel sample order do not depend on N,
 so the assembled image is bit-identical to the 1-GPU image.
 """
@@ -32,6 +38,68 @@ def tile_rows(rank: int, world: int, H: int, band: int = BAND) -> int:
 def max_tile_rows(world: int, H: int, band: int = BAND) -> int:
     """Padded per-rank tile height: whole bands, the same for every rank."""
     return -(-H // (world * band)) * band
+
+
+def cost_bucket(costs):
+    """Quarter-octave cost buckets (the single-GPU schedule's sort key, trace.hip sort_tiles): -1 for 0."""
+    import numpy as np
+
+    c = np.asarray(costs, dtype=np.float64)
+    return np.where(c > 0, np.floor(4.0 * np.log2(np.maximum(c, 1.0))), -1.0)
+
+
+def balanced_tiles(costs, world: int) -> list:
+    """Deal the tiles of a layout to `world` ranks by their measured costs: tiles sorted by cost
+    (descending, ties by index) are dealt serpentine (0..N-1, N-1..0, ...), so the ranks' cost sums
+    differ by less than one tile's cost. Each rank's list is in dispatch order: longest first by
+    quarter-octave bucket, row-major inside a bucket (waves running together stay close in the
+    image). Deterministic: equal costs give equal partitions on every rank."""
+    import numpy as np
+
+    c = np.asarray(costs, dtype=np.int64)
+    n = len(c)
+    idx = np.arange(n, dtype=np.int64)
+    order = np.lexsort((idx, -c))
+    pos = np.arange(n, dtype=np.int64)
+    blk, w = pos // world, pos % world
+    owner = np.empty(n, dtype=np.int64)
+    owner[order] = np.where(blk % 2 == 0, w, world - 1 - w)
+    bucket = cost_bucket(c)
+    out = []
+    for r in range(world):
+        t = idx[owner == r]
+        t = t[np.lexsort((t, -bucket[t]))]
+        out.append(t.astype(np.int32))
+    return out
+
+
+def tile_pixels(tiles, tiles_x: int, tw: int, th: int, W: int, nrows: int):
+    """Flat pixel indices (row * W + col of the layout's output) of the tiles' pixels, tile by tile
+    (row-major inside a tile), clipped to the image."""
+    import numpy as np
+
+    t = np.asarray(tiles, dtype=np.int64)
+    tx, ty = t % tiles_x, t // tiles_x
+    dy, dx = np.divmod(np.arange(tw * th, dtype=np.int64), tw)
+    rows = ty[:, None] * th + dy[None, :]
+    cols = tx[:, None] * tw + dx[None, :]
+    ok = (rows < nrows) & (cols < W)
+    return (rows * W + cols)[ok]
+
+
+def tile_assembler(pix, cap: int, device):
+    """Rank 0's reassembly of gathered tile buffers: pix[r] = rank r's pixel indices (tile_pixels),
+    its packed pixels in slots [0, len(pix[r])) of its [cap, ...] buffer -> the flat image."""
+    import numpy as np
+    import torch
+
+    dst = torch.from_numpy(np.concatenate(pix)).to(device)
+    src = torch.from_numpy(np.concatenate([np.arange(len(x), dtype=np.int64) + r * cap
+                                           for r, x in enumerate(pix)])).to(device)
+
+    def assemble_into(g, img):
+        img.index_copy_(0, dst, g.reshape((-1,) + tuple(g.shape[2:])).index_select(0, src))
+    return assemble_into
 
 
 def assemble(gathered, H: int, band: int = BAND):
@@ -76,12 +144,15 @@ class FrameExchange:
     one render that way.
     """
 
-    def __init__(self, dist, H: int, tile_shape, device, dtype=None, band: int = BAND):
+    def __init__(self, dist, H: int, tile_shape, device, dtype=None, band: int = BAND, assemble_into=None):
+        """assemble_into(gathered, image): rank 0's reassembly of [world, *tile_shape] into the image
+        [H, *tile_shape[1:]] (default: the interleaved row bands, `assemble`)."""
         import torch
 
         dtype = dtype or torch.float32
         self.dist, self.H, self.band = dist, H, band
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.assemble_into = assemble_into
         self.tiles = [torch.zeros(tuple(tile_shape), dtype=dtype, device=device) for _ in range(2)]
         root = self.rank == 0
         self.gathered = torch.empty((self.world,) + tuple(tile_shape), dtype=dtype, device=device) if root else None
@@ -94,7 +165,10 @@ class FrameExchange:
             self._pending.wait()  # NCCL: the current stream waits for the gather; gloo: the host does
             self._pending = None
             if self.rank == 0:
-                self.image.copy_(assemble(self.gathered, self.H, self.band))
+                if self.assemble_into is not None:
+                    self.assemble_into(self.gathered, self.image)
+                else:
+                    self.image.copy_(assemble(self.gathered, self.H, self.band))
 
     def tile(self):
         """This frame's tile buffer (render into it, then post())."""
@@ -198,16 +272,20 @@ def build_photons_sharded(scene, seed: int, count: int, dist=None, device="cuda"
 
 
 class RankRenderer:
-    """One rank's share of bench.py's N-GPU step: renders the rank's row bands (rows_of) with
-    the HIP kernel into device tiles on the current stream (rt_render_device: float RGB and the
-    reference's ARGB ints, myObjShader.java:671), and with N > 1 hands the planes in `planes`
-    to a FrameExchange each (gathered to rank 0 and re-interleaved there, pipelined against the
-    next frame). The ARGB plane is the frame the reference produces (`rndrdImg.pixels`,
-    myScene.java:1171-1177): the kernel packs it from the double colour, so rank 0 receives the
-    1-GPU ints exactly (packing the gathered float RGB again could differ by one in a channel
-    whose double value rounds up to the next float). `stage_host`: copy the tiles to host
-    memory before the exchange (the gloo backend, which cannot gather device tensors; used to run
-    this exact path as several processes on one GPU).
+    """One rank's share of bench.py's N-GPU step: renders the rank's part of the frame with the HIP
+    kernel into device buffers on the current stream (float RGB and the reference's ARGB ints,
+    myObjShader.java:671), and with N > 1 hands the planes in `planes` to a FrameExchange each
+    (gathered to rank 0 and reassembled there, pipelined against the next frame). The ARGB plane is
+    the frame the reference produces (`rndrdImg.pixels`, myScene.java:1171-1177): the kernel packs it
+    from the double colour, so rank 0 receives the 1-GPU ints exactly (packing the gathered float RGB
+    again could differ by one in a channel whose double value rounds up to the next float).
+
+    partition "tiles" (default): the frame's wave tiles dealt by measured cost (`balanced_tiles`;
+    rank 0 calibrates, rt_tile_costs, and broadcasts the costs); rank r renders its tile list into a
+    whole-frame buffer (rt_render_tiles_device) and packs its pixels (`tile_pixels`) for the gather.
+    partition "bands": the interleaved 8-row bands of `rows_of` (rt_render_device).
+    `stage_host`: copy the tiles to host memory before the exchange (the gloo backend, which cannot
+    gather device tensors; used to run this exact path as several processes on one GPU).
 
       rr = RankRenderer(scene, W, H, spp, seed, dist)
       rr.calibrate()                 # untimed: the layout's tile-schedule calibration renders
@@ -216,44 +294,75 @@ class RankRenderer:
                                      # [H, W] int32 (device / host; None for a plane not exchanged)
     """
 
-    def __init__(self, scene, W, H, spp, seed, dist=None, stage_host=False, band=BAND, planes=("rgb", "argb")):
+    def __init__(self, scene, W, H, spp, seed, dist=None, stage_host=False, band=BAND, planes=("rgb", "argb"),
+                 partition="tiles"):
+        import numpy as np
         import torch
 
         from . import rt
 
+        assert partition in ("tiles", "bands")
+        assert set(planes) <= {"rgb", "argb"} and planes
         self.scene, self.W, self.H = scene, W, H
         self.dist = dist
         self.rank = dist.get_rank() if dist else 0
         self.world = dist.get_world_size() if dist else 1
-        r0, r1, step, b = rows_of(self.rank, self.world, H, band)
-        self.p = rt.params(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=step, row_band=b)
-        self.rows = (r0, r1, step, b)
-        self.maxrows = max_tile_rows(self.world, H, band)
-        assert rt.nrows_of(self.p) <= self.maxrows
-        assert set(planes) <= {"rgb", "argb"} and planes
-        self.rgb = torch.empty((self.maxrows, W, 3), dtype=torch.float32, device="cuda")
-        self.argb = torch.empty((self.maxrows, W), dtype=torch.int32, device="cuda")
+        self.partition = partition if self.world > 1 else "bands"
         self.stream = torch.cuda.current_stream()
         self.stage_host = stage_host
         self.ex = {}
-        if dist is not None and self.world > 1:
-            dev = "cpu" if stage_host else "cuda"
-            if "rgb" in planes:
-                self.ex["rgb"] = FrameExchange(dist, H, (self.maxrows, W, 3), dev, band=band)
-            if "argb" in planes:
-                self.ex["argb"] = FrameExchange(dist, H, (self.maxrows, W), dev, dtype=torch.int32, band=band)
+        xdev = "cpu" if stage_host else "cuda"  # where the exchanged tiles (and collectives' tensors) live
+        if self.partition == "bands":
+            r0, r1, step, b = rows_of(self.rank, self.world, H, band)
+            self.p = rt.params(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=step, row_band=b)
+            self.rows = (r0, r1, step, b)
+            self.maxrows = max_tile_rows(self.world, H, band)
+            assert rt.nrows_of(self.p) <= self.maxrows
+            self.rgb = torch.empty((self.maxrows, W, 3), dtype=torch.float32, device="cuda")
+            self.argb = torch.empty((self.maxrows, W), dtype=torch.int32, device="cuda")
+            if dist is not None and self.world > 1:
+                if "rgb" in planes:
+                    self.ex["rgb"] = FrameExchange(dist, H, (self.maxrows, W, 3), xdev, band=band)
+                if "argb" in planes:
+                    self.ex["argb"] = FrameExchange(dist, H, (self.maxrows, W), xdev, dtype=torch.int32, band=band)
+            return
+        # cost-balanced tiles of the whole-frame layout
+        self.p = rt.params(W, H, spp=spp, seed=seed)
+        self.rows = (0, H, 1, 1)
+        ntiles, tiles_x, tw, th = scene.tile_layout(self.p)
+        cost = torch.zeros(ntiles, dtype=torch.int64, device=xdev)
+        if self.rank == 0:
+            cost.copy_(torch.from_numpy(scene.tile_costs(self.p).astype(np.int64)))
+        dist.broadcast(cost, 0)
+        parts = balanced_tiles(cost.cpu().numpy(), self.world)
+        self.tiles = parts[self.rank]
+        pix = [tile_pixels(t, tiles_x, tw, th, W, H) for t in parts]
+        self.npix = len(pix[self.rank])
+        self.pix = torch.from_numpy(pix[self.rank]).to("cuda")
+        cap = max(len(x) for x in pix)
+        self.rgb = torch.empty((H * W, 3), dtype=torch.float32, device="cuda")
+        self.argb = torch.empty((H * W,), dtype=torch.int32, device="cuda")
+        assemble_into = tile_assembler(pix, cap, xdev) if self.rank == 0 else None
+        if "rgb" in planes:
+            self.ex["rgb"] = FrameExchange(dist, H * W, (cap, 3), xdev, assemble_into=assemble_into)
+        if "argb" in planes:
+            self.ex["argb"] = FrameExchange(dist, H * W, (cap,), xdev, dtype=torch.int32, assemble_into=assemble_into)
 
     def render(self, rgb=None, argb=None, ev=None):
         if ev:
             ev[0].record(self.stream)
         rgb = self.rgb if rgb is None else rgb
         argb = self.argb if argb is None else argb
-        self.scene.render_device(self.p, rgb.data_ptr(), argb.data_ptr(), self.stream.cuda_stream)
+        if self.partition == "tiles":
+            self.scene.render_tiles_device(self.p, self.tiles, rgb.data_ptr(), argb.data_ptr(), self.stream.cuda_stream)
+        else:
+            self.scene.render_device(self.p, rgb.data_ptr(), argb.data_ptr(), self.stream.cuda_stream)
         if ev:
             ev[1].record(self.stream)
 
     def calibrate(self, n=2):
-        """A row layout's first two renders order its tiles (probe, then measured wave times)."""
+        """A row layout's first two renders order its tiles (probe, then measured wave times); a tile
+        partition was calibrated at construction (these renders only warm up)."""
         import torch
 
         for _ in range(n):
@@ -265,7 +374,16 @@ class RankRenderer:
             self.render(ev=ev)
             return
         tiles = {k: e.tile() for k, e in self.ex.items()}
-        if self.stage_host:
+        if self.partition == "tiles":
+            import torch
+
+            self.render(ev=ev)
+            for k, t in tiles.items():  # this rank's pixels, packed in tile order (device gather)
+                if self.stage_host:  # device -> host (synchronous), then the gloo gather
+                    t[: self.npix].copy_(torch.index_select(getattr(self, k), 0, self.pix))
+                else:
+                    torch.index_select(getattr(self, k), 0, self.pix, out=t[: self.npix])
+        elif self.stage_host:
             self.render(ev=ev)
             for k, t in tiles.items():
                 t.copy_(getattr(self, k))  # device -> host (synchronous), then the gloo gather
@@ -279,7 +397,13 @@ class RankRenderer:
         [H, W]; None for a plane not exchanged), the other ranks (None, None)."""
         if self.ex:
             out = {k: e.finish() for k, e in self.ex.items()}
-            return out.get("rgb"), out.get("argb")
+            if self.rank != 0:
+                return None, None
+            rgb, argb = out.get("rgb"), out.get("argb")
+            if self.partition == "tiles":
+                rgb = rgb.reshape(self.H, self.W, 3) if rgb is not None else None
+                argb = argb.reshape(self.H, self.W) if argb is not None else None
+            return rgb, argb
         if self.rank != 0:
             return None, None
         return self.rgb[: self.H], self.argb[: self.H]

@@ -46,7 +46,8 @@ EXPORTS = ["rt_abi_version", "rt_build_id", "rt_last_error", "rt_device_count", 
            "rt_render_count", "rt_time_render", "rt_render_pass", "rt_refine_steps", "rt_scene_photons",
            "rt_scene_photon_map", "rt_photons_shoot",
            "rt_photons_set",
-           "rt_png_name", "rt_scene_save_name", "rt_math_eval"]
+           "rt_png_name", "rt_scene_save_name", "rt_math_eval", "rt_tile_layout", "rt_tile_costs",
+           "rt_render_tiles_device", "rt_render_tiles_count"]
 
 _lib = None
 
@@ -95,6 +96,12 @@ def lib():
                                        ctypes.c_void_p, ctypes.c_void_p]
         L.rt_time_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_double)]
+        L.rt_tile_layout.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p]
+        L.rt_tile_costs.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int]
+        L.rt_render_tiles_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.rt_render_tiles_count.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_void_p]
         L.rt_math_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
         L.rt_png_name.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
         L.rt_scene_save_name.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
@@ -287,6 +294,35 @@ class Scene:
         """Asynchronous render into device buffers (e.g. torch tensors' data_ptr()) on a HIP stream."""
         _check(lib().rt_render_device(self._h, ctypes.byref(p), ctypes.c_void_p(rgb_ptr), ctypes.c_void_p(argb_ptr),
                                       ctypes.c_void_p(stream)), "rt_render_device")
+
+    def tile_layout(self, p: RenderParams) -> tuple[int, int, int, int]:
+        """(ntiles, tiles_x, tw, th) of a render layout (rt_tile_layout)."""
+        out = np.zeros(4, dtype=np.int32)
+        _check(lib().rt_tile_layout(self._h, ctypes.byref(p), out.ctypes.data), "rt_tile_layout")
+        return tuple(int(x) for x in out)
+
+    def tile_costs(self, p: RenderParams) -> np.ndarray:
+        """Measured wave time of every tile of the layout (uint32 [ntiles]; calibrates if needed)."""
+        n = self.tile_layout(p)[0]
+        c = np.zeros(n, dtype=np.uint32)
+        r = lib().rt_tile_costs(self._h, ctypes.byref(p), c.ctypes.data, n)
+        if r < 0:
+            raise RTError(f"rt_tile_costs failed ({r}): {lib().rt_last_error().decode()}")
+        return c
+
+    def render_tiles_device(self, p: RenderParams, tiles: np.ndarray, rgb_ptr: int, argb_ptr: int, stream: int = 0):
+        """Asynchronous render of the listed tiles (host int32 list) into whole-layout device buffers."""
+        t = np.ascontiguousarray(tiles, dtype=np.int32)
+        _check(lib().rt_render_tiles_device(self._h, ctypes.byref(p), t.ctypes.data, len(t), ctypes.c_void_p(rgb_ptr),
+                                            ctypes.c_void_p(argb_ptr), ctypes.c_void_p(stream)), "rt_render_tiles_device")
+
+    def render_tiles_count(self, p: RenderParams, tiles: np.ndarray) -> dict:
+        """Counters (rt_render_count's) of an instrumented render of the listed tiles only."""
+        t = np.ascontiguousarray(tiles, dtype=np.int32)
+        st = np.zeros(RT_ST_N, dtype=np.uint64)
+        _check(lib().rt_render_tiles_count(self._h, ctypes.byref(p), t.ctypes.data, len(t), st.ctypes.data),
+               "rt_render_tiles_count")
+        return dict(zip(ST_NAMES, st[: len(ST_NAMES)].tolist()))
 
     def time_render(self, W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, warmup=1, iters=3, flags=0,
                     row_band=1) -> float:

@@ -259,6 +259,23 @@ int rt_render(rt_scene* scene, const rt_render_params* p, float* rgb, int32_t* a
    and records its waves' durations; the next render of that layout synchronises once and orders the
    tiles by those measured times (longest first). Render a layout twice before timing it. */
 int rt_render_device(rt_scene* scene, const rt_render_params* p, float* d_rgb, int32_t* d_argb, void* hip_stream);
+/* Tile partitions (multi-GPU). A render layout (p's size, rows and spp) is cut into
+   wave tiles of tw x th pixels, numbered row-major over tiles_x columns of tiles.
+   rt_tile_layout: out[0..3] = {ntiles, tiles_x, tw, th}.
+   rt_tile_costs: the measured wave time of every tile of the layout (calibrating the layout first if no
+   render of it has measured its waves; synchronous) into cost[min(ntiles, cap)]; returns ntiles.
+   Layouts under 2^16 pixels are not scheduled (row-major dispatch): every tile costs 1.
+   rt_render_tiles_device: render only the tiles tiles[0..ntiles) (a HOST int32 list, each < the
+   layout's ntiles, dispatched in that order; validated and copied to the device once per distinct
+   list, the last 16 kept) asynchronously on hip_stream into DEVICE buffers of the WHOLE layout (rgb float[n_rows*width*3], argb int32[n_rows*width]; pixels of other tiles are not written).
+   Pixels do not depend on which tiles a launch holds: a partition of the tiles over N launches (or N
+   GPUs) reassembles to the 1-launch image bit for bit. */
+int rt_tile_layout(rt_scene* scene, const rt_render_params* p, int32_t* out);
+int rt_tile_costs(rt_scene* scene, const rt_render_params* p, uint32_t* cost, int cap);
+int rt_render_tiles_device(rt_scene* scene, const rt_render_params* p, const int32_t* tiles, int ntiles, float* d_rgb,
+                           int32_t* d_argb, void* hip_stream);
+/* Instrumented render of the listed tiles (rt_render_count's counters for those tiles only; blocking). */
+int rt_render_tiles_count(rt_scene* scene, const rt_render_params* p, const int32_t* tiles, int ntiles, uint64_t* stats);
 /* `refine on` (myScene.setRefine, myScene.java:796-803): the progressive steps of a width x height
    render, largest first and ending at 1 (e.g. 16 8 4 2 1 at 300x300); returns their number n and
    copies min(n, cap) of them; n = 1 (steps {1}) when the scene does not refine. */

@@ -2,9 +2,9 @@
 configs[4]), which the parity tests otherwise cover only at reduced size:
 
 * deterministic: two renders are bit-equal;
-* the N-GPU partition: the eight row-band tiles of an 8-rank split (multigpu.rows_of, the
-  layout bench.py --gpus 8 runs) padded, stacked and re-interleaved with multigpu.assemble
-  equal the 1-GPU frame bit for bit, float RGB and ARGB alike;
+* the N-GPU partitions: the eight cost-balanced tile lists of an 8-rank split (the layout
+  bench.py --gpus 8 runs) and the eight row-band tiles (multigpu.rows_of, --partition bands)
+  reassemble to the 1-GPU frame bit for bit, float RGB and ARGB alike;
 * parity: a row subsample of the full frame against the oracle at the full spp, with the
   decision-exact bar of tests/parity.py (per-channel |d| <= 1e-4 where decisions agree, 0
   decision mismatches, ARGB equal).
@@ -38,6 +38,30 @@ def _split_equals_full(g, W, H, spp, seed, rgb, argb, world=8):
     assert np.array_equal(multigpu.assemble(tr, H).view(np.uint32), rgb.view(np.uint32))
 
 
+def _tiles_split_equals_full(g, W, H, spp, seed, rgb, argb, world=8):
+    """The cost-balanced tile partition of bench.py --gpus 8 (measured costs, balanced_tiles,
+    rt_render_tiles_device per rank, pixels scattered back by tile_pixels) == the 1-GPU frame."""
+    import torch
+
+    p = rt.params(W, H, spp=spp, seed=seed)
+    n, tx, tw, th = g.tile_layout(p)
+    parts = multigpu.balanced_tiles(g.tile_costs(p), world)
+    assert sum(len(t) for t in parts) == n
+    out_rgb = torch.full((H * W, 3), -1.0, device="cuda")
+    out_argb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    b_rgb, b_argb = torch.empty_like(out_rgb), torch.empty_like(out_argb)
+    st = torch.cuda.current_stream()
+    for t in parts:
+        b_rgb.fill_(-2.0)
+        g.render_tiles_device(p, t, b_rgb.data_ptr(), b_argb.data_ptr(), st.cuda_stream)
+        pix = torch.from_numpy(multigpu.tile_pixels(t, tx, tw, th, W, H)).cuda()
+        out_rgb[pix] = b_rgb[pix]
+        out_argb[pix] = b_argb[pix]
+    torch.cuda.synchronize()
+    assert np.array_equal(out_argb.cpu().numpy().reshape(H, W), argb)
+    assert np.array_equal(out_rgb.cpu().numpy().reshape(H, W, 3).view(np.uint32), rgb.view(np.uint32))
+
+
 def test_c4_full_size_properties():
     cli, W, H, spp, seed = scenes.CONFIGS["C4"]
     scenes.ensure_bun69k()
@@ -48,6 +72,7 @@ def test_c4_full_size_properties():
     assert np.array_equal(argb, argb2) and np.array_equal(rgb.view(np.uint32), rgb2.view(np.uint32))
     assert rgb.min() >= 0 and rgb.max() <= 1.0
     _split_equals_full(g, W, H, spp, seed, rgb, argb)
+    _tiles_split_equals_full(g, W, H, spp, seed, rgb, argb)
     # oracle rows through the glass bunnies, the columns and the sky (the oracle runs ~3 s a row)
     o = OracleScene(scenes.SCENE_DIR, cli, tex)
     for row in (700, 1300, 1900):
@@ -65,6 +90,7 @@ def test_c5_full_size_properties():
     assert np.array_equal(argb, argb2) and np.array_equal(rgb.view(np.uint32), rgb2.view(np.uint32))
     assert rgb.min() >= 0 and rgb.max() <= 1.0
     _split_equals_full(g, W, H, spp, seed, rgb, argb)
+    _tiles_split_equals_full(g, W, H, spp, seed, rgb, argb)
     o = OracleScene(scenes.SCENE_DIR, cli)
     o.set_photons(*g.photons())
     for row in (100, 400, 640, 900):  # ceiling light, spheres (mirror / glass: caustics), floor

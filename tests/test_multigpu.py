@@ -205,3 +205,93 @@ def test_merge_photon_shards_restores_insertion_order():
     mp, mw = multigpu.merge_photon_shards(shards)
     assert np.array_equal(mp, pos_full) and np.array_equal(mw, pos_full * 2)
     assert sum(multigpu.photon_shard(r, 3, 10)[1] for r in range(3)) == 10
+
+
+def test_balanced_tiles_partition():
+    """Cost-balanced tile partition (multigpu.balanced_tiles): every tile exactly once, the same
+    partition for the same costs, cost sums within one tile's cost of each other, and each rank's
+    list longest-first by quarter-octave bucket (row-major inside a bucket)."""
+    rng = np.random.default_rng(7)
+    for n, world in [(1000, 2), (262144, 8), (37, 3), (5, 8)]:
+        costs = (rng.pareto(1.5, n) * 1000 + 1).astype(np.uint32)
+        costs[rng.random(n) < 0.05] = costs[0]  # ties
+        parts = multigpu.balanced_tiles(costs, world)
+        assert len(parts) == world
+        allt = np.concatenate(parts)
+        assert np.array_equal(np.sort(allt), np.arange(n))
+        again = multigpu.balanced_tiles(costs.copy(), world)
+        assert all(np.array_equal(a, b) for a, b in zip(parts, again))
+        sums = [int(costs[p].astype(np.int64).sum()) for p in parts]
+        assert max(sums) - min(sums) <= int(costs.max())
+        b = multigpu.cost_bucket(costs)
+        for p in parts:
+            kb = b[p]
+            assert np.all(np.diff(kb) <= 0)
+            same = np.diff(kb) == 0
+            assert np.all(np.diff(p)[same] > 0)
+
+
+def test_tile_pixels_cover_the_image():
+    """The tiles of a layout (tw x th pixel wave tiles, clipped at the image edge) cover every
+    pixel exactly once, whatever the partition."""
+    for W, H, tw, th in [(1024, 1024, 2, 2), (37, 19, 2, 2), (10, 7, 1, 1), (13, 9, 8, 8)]:
+        tx = -(-W // tw)
+        n = tx * -(-H // th)
+        parts = multigpu.balanced_tiles(np.arange(n)[::-1] % 17 + 1, 3)
+        pix = np.concatenate([multigpu.tile_pixels(t, tx, tw, th, W, H) for t in parts])
+        assert np.array_equal(np.sort(pix), np.arange(W * H))
+
+
+def _tiles_worker(rank, world, port, W, H, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tw, th = 2, 2
+    tx = -(-W // tw)
+    n = tx * -(-H // th)
+    cost = torch.zeros(n, dtype=torch.int64)
+    if rank == 0:  # only rank 0 measures (RankRenderer: rt_tile_costs), the others receive them
+        cost.copy_(torch.from_numpy((np.arange(n) * 7919 % 1000 + 1).astype(np.int64)))
+    dist.broadcast(cost, 0)
+    parts = multigpu.balanced_tiles(cost.numpy(), world)
+    pix = [multigpu.tile_pixels(t, tx, tw, th, W, H) for t in parts]
+    cap = max(len(x) for x in pix)
+    mine = torch.from_numpy(pix[rank])
+    asm = multigpu.tile_assembler(pix, cap, "cpu") if rank == 0 else None
+    ex = multigpu.FrameExchange(dist, H * W, (cap, 3), "cpu", assemble_into=asm)
+    frames = []
+    for f in range(3):
+        # the rank's "render": a whole-frame buffer where only its own tiles' pixels are right
+        full = torch.full((H * W, 3), -1.0)
+        full[mine] = (torch.arange(H * W, dtype=torch.float32)[mine] + 1000 * f)[:, None]
+        t = ex.tile()
+        t.zero_()
+        torch.index_select(full, 0, mine, out=t[: len(mine)])
+        ex.post()
+        if rank == 0 and f > 0:
+            frames.append(ex.image[:, 0].clone())
+    last = ex.finish()
+    if rank == 0:
+        frames.append(last[:, 0].clone())
+        q.put(torch.stack(frames).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world3_tile_partition_reassembles():
+    """The N-rank tile path (RankRenderer partition="tiles"): costs broadcast from rank 0, the same
+    partition on every rank, each rank's pixels packed in tile order, gathered and scattered back
+    by rank 0 -- every pixel of every frame in place (ragged image, unequal tile counts)."""
+    W, H, world = 37, 19, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_tiles_worker, args=(r, world, port, W, H, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    frames = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = np.stack([np.arange(H * W) + 1000 * f for f in range(3)]).astype(np.float32)
+    assert np.array_equal(frames, expect)

@@ -41,13 +41,16 @@ def _run(args, nproc, tmp, name):
     return d["rgb"], d["argb"]
 
 
+@pytest.mark.parametrize("partition", ["tiles", "bands"])
 @pytest.mark.parametrize("args", [
     ["--cli", "c3_bun69k.cli", "--size", "256", "--spp", "4"],
     ["--cli", "t11.cli", "--size", "96", "--spp", "2", "--seed", str(0x5EED0005)],  # sharded photon pre-pass
 ], ids=["c3", "t11_photons"])
-def test_two_rank_step_equals_one_rank_image(tmp_path, args):
+def test_two_rank_step_equals_one_rank_image(tmp_path, args, partition):
+    """Cost-balanced tiles (the default: rank 0's measured costs broadcast, rt_render_tiles_device,
+    pixels packed / scattered) and interleaved bands."""
     one, one_argb = _run(args, 1, tmp_path, "one")
-    two, two_argb = _run(args, 2, tmp_path, "two")
+    two, two_argb = _run(args + ["--partition", partition], 2, tmp_path, "two")
     assert one.shape == two.shape
     assert np.array_equal(one.view(np.uint32), two.view(np.uint32))
     # the reference's output, rndrdImg.pixels (myObjShader.java:671): rank 0's assembled ARGB

@@ -1,28 +1,69 @@
 #!/usr/bin/env python3
-"""Per-rank kernel time of the multi-GPU row-band partition, emulated on one GPU: max over
-ranks vs full-frame/N (strong-scaling efficiency of the kernel alone), with the probed
-longest-first tile schedule and with row-major dispatch."""
+"""Per-rank kernel time of the multi-GPU partitions, emulated on one GPU: max over ranks vs
+full-frame/N (strong-scaling efficiency of the kernel alone).
+
+  tools/band_timing.py [BANDS] [CFG] [--tiles] [--worlds 2,4,8]
+
+bands: rank r renders the interleaved row bands of multigpu.rows_of (rt_render_device, longest-
+first measured tile schedule of its own layout); --tiles: the cost-balanced tile lists of
+multigpu.balanced_tiles over the whole frame's measured wave times (rt_render_tiles_device, what
+bench.py --gpus N runs by default), each timed with HIP events on the launch stream."""
 import sys
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from distraytracer_old_amd import multigpu, rt, scenes  # noqa: E402
 
-BANDS = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [multigpu.BAND]
-ORDERS = ((0, "schedule"), (rt.RENDER_ROWMAJOR, "row-major")) if len(sys.argv) <= 1 else ((0, "schedule"),)
-CFG = sys.argv[2] if len(sys.argv) > 2 else "C3"  # tools/band_timing.py 8 C4
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+TILES = "--tiles" in sys.argv
+WORLDS = [2, 4, 8]
+if "--worlds" in sys.argv:
+    WORLDS = [int(x) for x in sys.argv[sys.argv.index("--worlds") + 1].split(",")]
+    args = [a for a in args if a != sys.argv[sys.argv.index("--worlds") + 1]]
+BANDS = [int(x) for x in args[0].split(",")] if args else [multigpu.BAND]
+CFG = args[1] if len(args) > 1 else "C3"
+ORDERS = ((0, "schedule"), (rt.RENDER_ROWMAJOR, "row-major")) if not args and not TILES else ((0, "schedule"),)
 cli, W, H, spp, seed = scenes.CONFIGS[CFG]
 scenes.ensure_bun69k()
 s = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
 s.build_photons(seed)
+
+
+def time_tiles(p, tiles, iters=5, warm=2):
+    import torch
+
+    rgb = torch.empty((H * W, 3), dtype=torch.float32, device="cuda")
+    argb = torch.empty((H * W,), dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream()
+    for _ in range(warm):
+        s.render_tiles_device(p, tiles, rgb.data_ptr(), argb.data_ptr(), st.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        s.render_tiles_device(p, tiles, rgb.data_ptr(), argb.data_ptr(), st.cuda_stream)
+    e1.record(st)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
 for flags, name in ORDERS:
     full = s.time_render(W, H, spp=spp, seed=seed, iters=5, flags=flags)
-    print(CFG, name, "full %.3f ms" % full)
-    for band, world in [(b, w) for b in BANDS for w in (2, 4, 8)]:
+    print(CFG, name, "full %.3f ms" % full, flush=True)
+    if TILES:
+        p = rt.params(W, H, spp=spp, seed=seed)
+        costs = s.tile_costs(p)
+        for world in WORLDS:
+            ts = [time_tiles(p, t) for t in multigpu.balanced_tiles(costs, world)]
+            print(" ", "tiles N", world, "max %.3f mean %.3f ideal %.3f eff %.3f" % (
+                max(ts), sum(ts) / len(ts), full / world, full / world / max(ts)),
+                "per rank", " ".join("%.3f" % t for t in ts), flush=True)
+        continue
+    for band, world in [(b, w) for b in BANDS for w in WORLDS]:
         ts = []
         for rank in range(world):
             r0, r1, step, b = multigpu.rows_of(rank, world, H, band)
             ts.append(s.time_render(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=step, row_band=b,
                                     iters=5, flags=flags))
-        print(" ", "band", band, "N", world, "max %.3f mean %.3f ideal %.3f eff %.3f" % (max(ts), sum(ts) / len(ts), full / world,
-                                                                       full / world / max(ts)))
+        print(" ", "band", band, "N", world, "max %.3f mean %.3f ideal %.3f eff %.3f" % (
+            max(ts), sum(ts) / len(ts), full / world, full / world / max(ts)),
+            "per rank", " ".join("%.3f" % t for t in ts), flush=True)

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""bench.py's N-rank step path, run for a check: every rank renders its row bands with the HIP
-kernel (multigpu.RankRenderer -> rt_render_device), the photon pre-pass (photon scenes) is
+"""bench.py's N-rank step path, run for a check: every rank renders its cost-balanced tiles
+(--partition tiles: rt_render_tiles_device) or row bands (bands: rt_render_device) with the HIP
+kernel (multigpu.RankRenderer), the photon pre-pass (photon scenes) is
 sharded over the ranks (multigpu.build_photons_sharded), the float-RGB and ARGB tiles go through
 multigpu.FrameExchange to rank 0, and rank 0 writes the assembled frame to --out (.npz: rgb, argb).
 
@@ -24,6 +25,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0x5EED0001)
     ap.add_argument("--frames", type=int, default=3)
     ap.add_argument("--backend", default="gloo", choices=["gloo", "nccl"])
+    ap.add_argument("--partition", default="tiles", choices=["tiles", "bands"])
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -50,14 +52,16 @@ def main():
     if info["photon_mode"]:
         multigpu.build_photons_sharded(scene, a.seed, info["photon_count"], dist,
                                        device="cuda" if a.backend == "nccl" else "cpu")
-    rr = multigpu.RankRenderer(scene, a.size, a.size, a.spp, a.seed, dist, stage_host=(a.backend == "gloo"))
+    rr = multigpu.RankRenderer(scene, a.size, a.size, a.spp, a.seed, dist, stage_host=(a.backend == "gloo"),
+                               partition=a.partition)
     rr.calibrate()
     frames = []
     for _ in range(a.frames):
         rr.step()
         ex = rr.ex.get("rgb") if rr.ex else None
         if ex is not None and rr.rank == 0 and ex.frame > 1:  # the previous frame, assembled
-            frames.append((ex.image.cpu().numpy().copy(), rr.ex["argb"].image.cpu().numpy().copy()))
+            frames.append((ex.image.cpu().numpy().reshape(a.size, a.size, 3).copy(),
+                           rr.ex["argb"].image.cpu().numpy().reshape(a.size, a.size).copy()))
     rgb, argb = rr.finish()
     torch.cuda.synchronize()
     if rr.rank == 0:
