@@ -14,6 +14,7 @@
 // reference the device build is tested against (DISTRAYTRACER_PHOTON_BUILD=host).
 #include <algorithm>
 #include <cstring>
+#include <thread>
 #include <utility>
 
 #include "rt_internal.h"
@@ -72,7 +73,96 @@ struct PhotonBvh {
   }
 };
 
+// myKD_Tree.build_tree (myLight.java:332-381) over photon_list indices: a range of one photon is a
+// leaf; otherwise the axis of largest extent (mins / maxs from +-1e20, `dx >= dy && dx >= dz` -> x,
+// then y, then z), Collections.sort of the range on that coordinate -- stable, `<` / `>` compares,
+// so the previous order breaks ties and -0 ties +0 -- and the median at size / 2 becomes the node.
+// A range of m photons holds exactly m nodes, numbered in DFS pre-order: the left child of node q
+// is q + 1, the right one q + 1 + split. Subtrees near the root are built on their own threads.
+struct JavaKd {
+  const double* pos;
+  int32_t* idx;
+  KdNodeD* out;
+  void sort_range(int lo, int hi, int ax, std::vector<int32_t>& buf) const {
+    const int n = hi - lo;
+    int32_t* a = idx + lo;
+    auto key = [&](int32_t i) { return pos[3 * (size_t)i + ax]; };
+    if (n <= 24) {  // stable insertion sort
+      for (int i = 1; i < n; ++i) {
+        const int32_t v = a[i];
+        const double kv = key(v);
+        int j = i - 1;
+        while (j >= 0 && kv < key(a[j])) { a[j + 1] = a[j]; --j; }
+        a[j + 1] = v;
+      }
+      return;
+    }
+    // stable merge sort with a caller-owned buffer (no allocation per node)
+    buf.resize(n);
+    for (int w = 1; w < n; w *= 2) {
+      for (int l = 0; l < n; l += 2 * w) {
+        const int m = std::min(l + w, n), r = std::min(l + 2 * w, n);
+        int i = l, j = m, o = l;
+        while (i < m && j < r) buf[o++] = (key(a[j]) < key(a[i])) ? a[j++] : a[i++];
+        while (i < m) buf[o++] = a[i++];
+        while (j < r) buf[o++] = a[j++];
+      }
+      std::copy(buf.begin(), buf.begin() + n, a);
+    }
+  }
+  void build(int lo, int hi, int q, int depth) {
+    std::vector<int32_t> buf;
+    build_(lo, hi, q, depth, buf);
+  }
+  void build_(int lo, int hi, int q, int depth, std::vector<int32_t>& buf) {
+    const int n = hi - lo;
+    if (n == 1) {
+      out[q] = KdNodeD{idx[lo], -1, -1, -1};
+      return;
+    }
+    double mn[3] = {1e20, 1e20, 1e20}, mx[3] = {-1e20, -1e20, -1e20};
+    for (int i = lo; i < hi; ++i) {
+      const double* p = pos + 3 * (size_t)idx[i];
+      for (int c = 0; c < 3; ++c) {
+        if (p[c] < mn[c]) mn[c] = p[c];
+        if (p[c] > mx[c]) mx[c] = p[c];
+      }
+    }
+    const double dx = mx[0] - mn[0], dy = mx[1] - mn[1], dz = mx[2] - mn[2];
+    const int ax = (dx >= dy && dx >= dz) ? 0 : (dy >= dx && dy >= dz) ? 1 : 2;
+    sort_range(lo, hi, ax, buf);
+    const int split = n / 2;
+    const int qr = q + 1 + split;
+    out[q] = KdNodeD{idx[lo + split], ax, split != 0 ? q + 1 : -1, split != n - 1 ? qr : -1};
+    if (depth < 4 && n > 4096) {  // the two subtrees in parallel
+      std::thread t([this, lo, split, q, depth] { if (split != 0) build(lo, lo + split, q + 1, depth + 1); });
+      if (split != n - 1) build_(lo + split + 1, hi, qr, depth + 1, buf);
+      t.join();
+    } else {
+      if (split != 0) build_(lo, lo + split, q + 1, depth + 1, buf);
+      if (split != n - 1) build_(lo + split + 1, hi, qr, depth + 1, buf);
+    }
+  }
+};
+
 }  // namespace
+
+std::vector<KdNodeD> build_java_kdtree(const std::vector<double>& pos) {
+  const int n = (int)(pos.size() / 3);
+  std::vector<KdNodeD> out(n);
+  if (n == 0) return out;
+  std::vector<int32_t> idx(n);
+  for (int i = 0; i < n; ++i) idx[i] = i;
+  JavaKd b{pos.data(), idx.data(), out.data()};
+  b.build(0, n, 0, 0);
+  return out;
+}
+
+void kd_to_leaf_order(std::vector<KdNodeD>& kd, const std::vector<int32_t>& leafToList) {
+  std::vector<int32_t> leafOf(leafToList.size());
+  for (size_t i = 0; i < leafToList.size(); ++i) leafOf[leafToList[i]] = (int32_t)i;
+  for (KdNodeD& k : kd) k.photon = leafOf[k.photon];
+}
 
 void build_photon_tree(HostScene& hs, const std::vector<double>& pos, const std::vector<double>& pwr) {
   hs.photonListPos = pos;
@@ -99,6 +189,13 @@ void build_photon_tree(HostScene& hs, const std::vector<double>& pos, const std:
       hs.ppos[3 * (size_t)i + c] = pos[3 * (size_t)idx[i] + c];
       hs.ppwr[3 * (size_t)i + c] = pwr[3 * (size_t)idx[i] + c];
     }
+  // the reference's kd-tree after the BVH records (KdNodeD), photons as leaf-order indices
+  std::vector<KdNodeD> kd = build_java_kdtree(pos);
+  kd_to_leaf_order(kd, idx);
+  const size_t off = hs.pnode.size();
+  hs.pnode.resize(off + (kd.size() + KD_PER_NODED - 1) / KD_PER_NODED);
+  std::memcpy(&hs.pnode[off], kd.data(), kd.size() * sizeof(KdNodeD));
+  hs.pnode[hs.photonRoot].padR[2] = (int32_t)off;
 }
 
 }  // namespace rt

@@ -222,7 +222,8 @@ struct DevBuf {  // scratch allocations of one build, freed on every path
 
 // Build the photon map of photon_list (pos / pwr, insertion order) on the scene's device.
 // out: device arrays owned by the scene (allocs); n > PHOTON_LEAF.
-int build_photon_tree_gpu(rt_scene* s, const double* pos_h, const double* pwr_h, int64_t n64) {
+int build_photon_tree_gpu(rt_scene* s, const double* pos_h, const double* pwr_h, int64_t n64,
+                          std::future<std::vector<KdNodeD>>& kdF) {
   using namespace pb;
   const int32_t n = (int32_t)n64;
   const int TB = 256;
@@ -261,14 +262,15 @@ int build_photon_tree_gpu(rt_scene* s, const double* pos_h, const double* pwr_h,
   // results (scene-owned)
   NodeD* nodes = nullptr;
   double *ppos = nullptr, *ppwr = nullptr;
-  PBCHK(hipMalloc(&nodes, sizeof(NodeD) * nnodes));
+  const int64_t kdRecs = (n64 + KD_PER_NODED - 1) / KD_PER_NODED;  // the reference's kd-tree after the BVH
+  PBCHK(hipMalloc(&nodes, sizeof(NodeD) * (nnodes + kdRecs)));
   s->allocs.push_back(nodes);
   PBCHK(hipMalloc(&ppos, sizeof(double) * 3 * (size_t)n));
   s->allocs.push_back(ppos);
   PBCHK(hipMalloc(&ppwr, sizeof(double) * 3 * (size_t)n));
   s->allocs.push_back(ppwr);
-  s->devBytes += sizeof(NodeD) * nnodes + 2 * sizeof(double) * 3 * (size_t)n;
-  PBCHK(hipMemset(nodes, 0, sizeof(NodeD) * nnodes));
+  s->devBytes += sizeof(NodeD) * (nnodes + kdRecs) + 2 * sizeof(double) * 3 * (size_t)n;
+  PBCHK(hipMemset(nodes, 0, sizeof(NodeD) * (nnodes + kdRecs)));
   PBCHK(hipMemset(leafStart, 0, sizeof(int32_t) * n));
   PBCHK(hipMemcpy(pos, pos_h, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice));
   PBCHK(hipMemcpy(pwr, pwr_h, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice));
@@ -321,6 +323,15 @@ int build_photon_tree_gpu(rt_scene* s, const double* pos_h, const double* pwr_h,
   hipLaunchKernelGGL(k_gather, dim3(gn), dim3(TB), 0, 0, L[0], n, pos, pwr, ppos, ppwr);
   PBCHK(hipGetLastError());
   PBCHK(hipDeviceSynchronize());
+  {  // the reference's kd-tree (built on a host thread meanwhile), photons renumbered to leaf order
+    std::vector<int32_t> leafToList(n);
+    PBCHK(hipMemcpy(leafToList.data(), L[0], sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    std::vector<KdNodeD> kd = kdF.get();
+    kd_to_leaf_order(kd, leafToList);
+    PBCHK(hipMemcpy(nodes + nnodes, kd.data(), sizeof(KdNodeD) * kd.size(), hipMemcpyHostToDevice));
+    const int32_t off = (int32_t)nnodes;
+    PBCHK(hipMemcpy(&nodes[0].padR[2], &off, sizeof(int32_t), hipMemcpyHostToDevice));
+  }
   s->dev.pnode = nodes;
   s->dev.ppos = ppos;
   s->dev.ppwr = ppwr;

@@ -1,6 +1,7 @@
 // Internal host-side declarations shared by the loader, builder and HIP launch code.
 #pragma once
 #include <cstring>
+#include <future>
 #include <string>
 #include <vector>
 
@@ -52,13 +53,19 @@ struct HostScene {
 int build_host_scene(const rt_scene_desc* d, HostScene& hs);  // scene_build.cpp
 // photon.cpp: photon-map search structure from the photon_list in insertion order
 void build_photon_tree(HostScene& hs, const std::vector<double>& pos, const std::vector<double>& pwr);
+// photon.cpp: the reference's kd-tree (myKD_Tree.build_tree) over photon_list indices, and its
+// photons renumbered to the photon map's leaf order (leafToList[i] = list index of leaf slot i)
+std::vector<KdNodeD> build_java_kdtree(const std::vector<double>& pos);
+void kd_to_leaf_order(std::vector<KdNodeD>& kd, const std::vector<int32_t>& leafToList);
 
 }  // namespace rt
 
 struct rt_scene;
 namespace rt {
 // photon_build.hip: the same structure built on the scene's device (n > PHOTON_LEAF)
-int build_photon_tree_gpu(rt_scene* s, const double* pos, const double* pwr, int64_t n);
+// kd: the reference's kd-tree over photon_list indices (build_java_kdtree), stored after the BVH
+int build_photon_tree_gpu(rt_scene* s, const double* pos, const double* pwr, int64_t n,
+                          std::future<std::vector<KdNodeD>>& kd);
 }  // namespace rt
 
 struct rt_scene {

@@ -135,6 +135,16 @@ struct TexD {
 // the photon positions and powers as double[3] arrays in leaf order (csrc/photon.cpp). The k-nearest set a query finds does not depend on the
 // search structure, so this replaces the reference's one-photon-per-node kd-tree.
 static constexpr int PHOTON_LEAF = 24;
+// The reference's own photon search structure, myKD_Tree (myLight.java:300-381): one photon per
+// node, the median of its range after a stable sort on the axis of largest extent. Kept only for
+// the exact replay of find_near at a tied k-th distance (trace_kernels.h knn_java). Stored after the
+// photon BVH's NodeD records in the same allocation; the root record's padR[2] holds its offset in
+// NodeD records (0: none). photon: the photon's index in the leaf-ordered ppos / ppwr arrays.
+struct KdNodeD {
+  int32_t photon, axis, left, right;  // axis -1: a leaf; child -1: none
+};
+static_assert(sizeof(KdNodeD) == 16, "KdNodeD");
+static constexpr int KD_PER_NODED = (int)(sizeof(NodeD) / sizeof(KdNodeD));
 
 // device-side scene handle (all pointers are device pointers)
 struct SceneD {

@@ -716,6 +716,27 @@ int rt_math_eval(const double* x, double* out, int64_t n, int device) {
   return RT_OK;
 }
 
+int rt_photon_gather(rt_scene* s, const double* pts, double* out, int64_t n) {
+  if (!s || n < 0 || (n > 0 && (!pts || !out))) return set_error(RT_E_INVALID, "rt_photon_gather: bad arguments");
+  if (!s->photonsUploaded) return set_error(RT_E_INVALID, "rt_photon_gather: no photon map (rt_photons_build / rt_photons_set)");
+  if (n == 0) return RT_OK;
+  HIPCHK(hipSetDevice(s->device));
+  double *dp = nullptr, *dout = nullptr;
+  HIPCHK(hipMalloc(&dp, sizeof(double) * 3 * n));
+  hipError_t e = hipMalloc(&dout, sizeof(double) * 3 * n);
+  if (e == hipSuccess) e = hipMemcpy(dp, pts, sizeof(double) * 3 * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(dv::gather_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), dv::LDS_RENDER_BYTES, 0, s->dev, dp,
+                       dout, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(double) * 3 * n, hipMemcpyDeviceToHost);
+  (void)hipFree(dp);
+  (void)hipFree(dout);
+  if (e != hipSuccess) return set_error(RT_E_HIP, hipGetErrorString(e));
+  return RT_OK;
+}
+
 int rt_render_count(rt_scene* s, const rt_render_params* p, float* rgb, int32_t* argb, uint64_t* stats) {
   if (!stats) return set_error(RT_E_INVALID, "null stats");
   return render_host(s, p, rgb, argb, stats);
@@ -1048,7 +1069,10 @@ static int set_photon_map(rt_scene* s, std::vector<double>& pos, std::vector<dou
   const char* mode = std::getenv("DISTRAYTRACER_PHOTON_BUILD");
   if (n > PHOTON_LEAF && !(mode && std::string(mode) == "host")) {
     HIPCHK(hipSetDevice(s->device));
-    int rc = build_photon_tree_gpu(s, pos.data(), pwr.data(), n);
+    // the reference's kd-tree on a host thread while the device builds the BVH
+    std::future<std::vector<KdNodeD>> kd = std::async(std::launch::async, [&pos] { return build_java_kdtree(pos); });
+    int rc = build_photon_tree_gpu(s, pos.data(), pwr.data(), n, kd);
+    if (kd.valid()) kd.wait();  // an early error return left it running: it reads pos
     h.photonListPos.swap(pos);
     h.photonListPwr.swap(pwr);
     return rc;

@@ -1863,6 +1863,108 @@ DEVI void knn_hist_pass(const SceneD& S, const double* pos, double lo, double hi
   }
 }
 
+// Exact replay of the reference's neighbourhood for ONE lane whose k-th distance is tied (several
+// photons at the boundary distance, some in and some out): myKD_Tree.find_near (myLight.java:389-445)
+// over the reference's own kd-tree (KdNodeD, built on the host like build_tree :332-381) with its
+// java.util.PriorityQueue(reverseOrder) as JDK 8 sifts it -- an element moves up only past a strictly
+// smaller parent and down only past a strictly larger child (the right child only when strictly
+// larger than the left) -- so the photons evicted among equal distances are Java's; then
+// getIrradianceFromPhtnTree (myObjShader.java:441-458): the powers summed in poll order (farthest
+// first) over pi * (the first polled d2). The heap and the recursion's frames live in the wave's pkT
+// LDS levels (idle once the counting selection's final pass is done); the lane runs alone.
+static_assert(KNN_MAX * 12 + 64 * 4 <= PK_LDS * 64 * 8, "the replay's heap and frames fit the pkT levels");
+#ifndef RT_KNN_JAVA_CALL  // the replay as a real call: the hot variants' register allocation stays as it was
+#define RT_KNN_JAVA_CALL 1
+#endif
+#if RT_KNN_JAVA_CALL
+#define KNN_JAVA_FN __device__ __attribute__((noinline))
+#else
+#define KNN_JAVA_FN DEVI
+#endif
+KNN_JAVA_FN V knn_java_(const NodeD* pnode, const double* ppos, const double* ppwr, int32_t root, int K, double maxd2,
+                        double px, double py, double pz) {
+  const double pos[3] = {px, py, pz};
+  const int32_t off = pnode[root].padR[2];
+  if (off <= 0) return mk(0, 0, 0);  // no kd-tree (unreachable: every photon map carries one)
+  const KdNodeD* kd = reinterpret_cast<const KdNodeD*>(pnode + off);
+  lds_f64* hd = pkT();                               // queue: d2
+  lds_i32* hx = (lds_i32*)(pkT() + KNN_MAX);         // queue: photon (leaf order)
+  lds_i32* stk = hx + KNN_MAX;                       // frames: node << 2 | stage
+  int n = 0;
+  auto poll = [&]() {  // PriorityQueue.poll: the root goes, the last element sifts down from it
+    --n;
+    const double xd = hd[n];
+    const int32_t xi = hx[n];
+    if (n > 0) {
+      int k = 0;
+      const int half = n >> 1;
+      while (k < half) {
+        int c = 2 * k + 1;
+        const int r = c + 1;
+        if (r < n && hd[r] > hd[c]) c = r;
+        if (xd >= hd[c]) break;
+        hd[k] = hd[c]; hx[k] = hx[c];
+        k = c;
+      }
+      hd[k] = xd; hx[k] = xi;
+    }
+  };
+  int sp = 0;
+  stk[sp++] = 0;  // the root (node 0), stage 0
+  while (sp > 0) {
+    const int32_t fr = stk[sp - 1];
+    const int32_t node = fr >> 2;
+    int stage = fr & 3;
+    const KdNodeD kn = kd[node];
+    const double* ph = ppos + 3 * (size_t)kn.photon;
+    if (stage == 0) {
+      if (kn.axis != -1) {  // the near side first (findNearbyNodes :411-423)
+        const double delta = pos[kn.axis] - ph[kn.axis];
+        const int32_t nearc = delta < 0 ? kn.left : kn.right;
+        stk[sp - 1] = (node << 2) | 1;
+        if (nearc != -1) { stk[sp++] = nearc << 2; continue; }
+        stage = 1;
+      } else {
+        stage = 2;
+      }
+    }
+    if (stage == 1) {  // the far side if the split plane is nearer than the current radius
+      const double delta = pos[kn.axis] - ph[kn.axis], delta2 = delta * delta;
+      const int32_t farc = delta < 0 ? kn.right : kn.left;
+      stk[sp - 1] = (node << 2) | 2;
+      if (farc != -1 && delta2 < maxd2) { stk[sp++] = farc << 2; continue; }
+    }
+    // the node's own photon (:425-444)
+    const double dx = pos[0] - ph[0], dy = pos[1] - ph[1], dz = pos[2] - ph[2];
+    const double len2 = dx * dx + dy * dy + dz * dz;
+    if (len2 < maxd2) {
+      int k = n++;  // PriorityQueue.offer: sift up
+      while (k > 0) {
+        const int parent = (k - 1) >> 1;
+        if (hd[parent] >= len2) break;
+        hd[k] = hd[parent]; hx[k] = hx[parent];
+        k = parent;
+      }
+      hd[k] = len2; hx[k] = kn.photon;
+      if (n > K) poll();
+      if (n == K && hd[0] < maxd2) maxd2 = hd[0];
+    }
+    --sp;
+  }
+  if (n == 0) return mk(0, 0, 0);  // [null] -> 0 (Q20)
+  const double area = PI_F * hd[0];
+  V res = mk(0, 0, 0);
+  while (n > 0) {  // poll order: farthest first
+    const double* w = ppwr + 3 * (size_t)hx[0];
+    res.x += w[0]; res.y += w[1]; res.z += w[2];
+    poll();
+  }
+  return mk(res.x / area, res.y / area, res.z / area);
+}
+DEVI V knn_java(const SceneD& S, const double* pos) {
+  return knn_java_(S.pnode, S.ppos, S.ppwr, S.photonRoot, S.photonK, S.photonMaxD2, pos[0], pos[1], pos[2]);
+}
+
 template <bool CNT>
 DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
 #ifdef RT_KNN_HEAP
@@ -1975,6 +2077,7 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
   V res = mk(0, 0, 0);
   double rSq = 0;
   int n = 0;
+  int m = 0;  // window photons
   // window photon: keep the KNN_SHELL nearest, sorted (scan order breaks ties)
   auto shell_insert = [&](double xd, int32_t xi) {
 #pragma unroll
@@ -1993,7 +2096,6 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
     // does: the list then keeps the first KNN_SHELL, as the sorted shell would.
     lds_f64* ld = pkT() + __lane_id();
     lds_i32* li = (lds_i32*)(pkT() + KNN_SHELL * 64) + __lane_id();
-    int m = 0;
     photon_scan_any<CNT, true>(S, pos, all ? R2max : hi, ct, [&](double d2, int i, V w) {
       if (all || d2 < lo) {
         res.x += w.x; res.y += w.y; res.z += w.z;
@@ -2015,24 +2117,39 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
         n++;
       } else {
         shell_insert(d2, i);
+        m++;
       }
     });
   }
+  // a tie across the k-th position: window photons `need` and `need + 1` (1-based) at the same
+  // distance (or more window photons than the sorted shell holds: all at one distance). Which of
+  // them the reference keeps is its kd-tree order and heap layout: such a lane replays find_near.
+  bool tie = false;
   if (!all) {
     const int need = K - below;
+    double dLast = -1, dNext = -2;
 #pragma unroll
-    for (int k = 0; k < KNN_SHELL; ++k)
+    for (int k = 0; k < KNN_SHELL; ++k) {
       if (k < need && si[k] >= 0) {
         const double* w = S.ppwr + 3 * (size_t)si[k];
         res.x += w[0]; res.y += w[1]; res.z += w[2];
         rSq = sd[k];
         n++;
       }
+      if (k == need - 1) dLast = sd[k];
+      if (k == need) dNext = sd[k];
+    }
+    tie = need >= 1 && need < m && (m > KNN_SHELL || dLast == dNext);
   }
   PROF_ADD(t_kf, R_KNN_FINAL);
-  if (n == 0) return mk(0, 0, 0);  // [null] -> 0 (Q20)
-  const double area = PI_F * rSq;
-  return mk(res.x / area, res.y / area, res.z / area);
+  V out = mk(0, 0, 0);
+  if (n > 0) {
+    const double area = PI_F * rSq;
+    out = mk(res.x / area, res.y / area, res.z / area);
+  }
+  for (uint64_t tl = __ballot(tie); tl; tl &= tl - 1)  // the tied lanes, one at a time
+    if (__lane_id() == (unsigned)__builtin_ctzll(tl)) out = knn_java(S, pos);
+  return out;
 }
 
 // skydome background (myScene.java:1104-1149)
@@ -3166,6 +3283,19 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   }
 #endif
 }
+
+#ifndef RT_MINREG_TU
+// The photon gather alone (rt_photon_gather): lane i returns getIrradianceFromPhtnTree at point i
+// through the render kernel's gather (counting selection, packet scans, exact-tie replay).
+__global__ void __launch_bounds__(64) gather_kernel(SceneD S, const double* __restrict__ pts, double* __restrict__ out,
+                                                    int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  Counters ct;
+  const V ir = irradiance<false>(S, mk(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), ct);
+  out[3 * i] = ir.x; out[3 * i + 1] = ir.y; out[3 * i + 2] = ir.z;
+}
+#endif
 
 #if RT_SPLIT_TU && !defined(RT_MINREG_TU)
 extern template __global__ void render_kernel<false, 0u>(SceneD, ParamsD, float*, int32_t*, unsigned long long*);

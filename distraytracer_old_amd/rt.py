@@ -47,7 +47,7 @@ EXPORTS = ["rt_abi_version", "rt_build_id", "rt_last_error", "rt_device_count", 
            "rt_scene_photon_map", "rt_photons_shoot",
            "rt_photons_set",
            "rt_png_name", "rt_scene_save_name", "rt_math_eval", "rt_tile_layout", "rt_tile_costs",
-           "rt_render_tiles_device", "rt_render_tiles_count"]
+           "rt_render_tiles_device", "rt_render_tiles_count", "rt_photon_gather"]
 
 _lib = None
 
@@ -62,6 +62,14 @@ def lib():
     """Load the HIP library; raises RTError (never falls back) if it is absent."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: PyTorch ships its own libamdhip64 (soname libamdhip64.so.7,
+        # loaded by file name), and a process that loads ours (/opt/rocm's, same soname) first and
+        # torch's later holds two runtimes, the second of which sees no GPU. With torch imported
+        # first the library binds to the runtime already loaded (the soname matches).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         p = lib_path()
         if not p.exists():
             raise RTError(f"{p} is missing: build it with `python -m distraytracer_old_amd.build`")
@@ -102,6 +110,7 @@ def lib():
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.rt_render_tiles_count.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int,
                                             ctypes.c_void_p]
+        L.rt_photon_gather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         L.rt_math_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
         L.rt_png_name.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
         L.rt_scene_save_name.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
@@ -315,6 +324,13 @@ class Scene:
         t = np.ascontiguousarray(tiles, dtype=np.int32)
         _check(lib().rt_render_tiles_device(self._h, ctypes.byref(p), t.ctypes.data, len(t), ctypes.c_void_p(rgb_ptr),
                                             ctypes.c_void_p(argb_ptr), ctypes.c_void_p(stream)), "rt_render_tiles_device")
+
+    def photon_gather(self, pts) -> np.ndarray:
+        """The render kernel's photon gather at points pts [n, 3] -> irradiance [n, 3] (rt_photon_gather)."""
+        pts = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 3)
+        out = np.zeros_like(pts)
+        _check(lib().rt_photon_gather(self._h, pts.ctypes.data, out.ctypes.data, len(pts)), "rt_photon_gather")
+        return out
 
     def render_tiles_count(self, p: RenderParams, tiles: np.ndarray) -> dict:
         """Counters (rt_render_count's) of an instrumented render of the listed tiles only."""

@@ -298,6 +298,9 @@ int rt_time_render(rt_scene* scene, const rt_render_params* p, int warmup, int i
 /* Diagnostics: the device's fdlibm sin / cos / asin / acos (the sequences the trace kernels use,
    shared bit for bit with the CPU oracle) of x[0..n) into out[4*i .. 4*i+3], host buffers. */
 int rt_math_eval(const double* x, double* out, int64_t n, int device);
+/* Diagnostics: the render kernel's photon gather (getIrradianceFromPhtnTree, myObjShader.java:441-458)
+   at points pts[3*i..3*i+2] into out[3*i..3*i+2] (host buffers); needs the scene's photon map. */
+int rt_photon_gather(rt_scene* scene, const double* pts, double* out, int64_t n);
 
 #ifdef __cplusplus
 }
