@@ -103,4 +103,9 @@ struct rt_scene {
     int32_t* dev = nullptr;
   };
   std::vector<TileList> tileLists;
+  // RT_RENDER_WAVEFRONT buffers (grow-only): level-0 records, sample colours, traced flags, level
+  // counters, two ray queues, the records of levels 1..7
+  enum { WF_NODE0, WF_SCOL, WF_TRACED, WF_CNT, WF_Q0, WF_Q1, WF_NODE1, WF_N = WF_NODE1 + 7 };
+  void* wf[WF_N] = {};
+  size_t wfCap[WF_N] = {};
 };

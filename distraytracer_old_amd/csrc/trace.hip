@@ -13,6 +13,7 @@
 
 #include "rt_internal.h"
 #include "trace_kernels.h"
+#include "wavefront.h"
 // ===========================================================================
 // host side: device upload + C ABI
 using namespace rt;
@@ -378,7 +379,7 @@ int rt_scene_photons(const rt_scene* s, double* pos, double* pwr, int64_t n, int
 
 void rt_scene_destroy(rt_scene* s) {
   if (!s) return;
-  if (!s->allocs.empty() || s->stream || s->outRgb || s->outArgb || !s->tileLists.empty() || s->stage) {
+  if (!s->allocs.empty() || s->stream || s->outRgb || s->outArgb || !s->tileLists.empty() || s->stage || s->wf[rt_scene::WF_CNT]) {
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize((hipStream_t)s->stream);
     for (void* p : s->allocs) (void)hipFree(p);
@@ -387,6 +388,7 @@ void rt_scene_destroy(rt_scene* s) {
     (void)hipFree(s->outRgb);
     (void)hipFree(s->outArgb);
     for (auto& t : s->tileLists) (void)hipFree(t.dev);
+    for (void* p : s->wf) (void)hipFree(p);
     if (s->stage) (void)hipHostFree(s->stage);
     if (s->stream) (void)hipStreamDestroy((hipStream_t)s->stream);
   }
@@ -587,12 +589,102 @@ static int schedule(rt_scene* s, ParamsD& P, bool count, hipStream_t st) {
   return RT_OK;
 }
 
+// ---------------------------------------------------------------------------
+// RT_RENDER_WAVEFRONT (wavefront.h): chunks of (tile, sample round) units, each traced level by
+// level -- one launch per generation of the shading tree over its compacted ray queue, the count of
+// the next level read back in between -- then folded bottom up and summed per pixel.
+#ifndef RT_WF_CHUNK
+#define RT_WF_CHUNK (1 << 24)  // camera samples per chunk
+#endif
+static int wf_grow(rt_scene* s, int i, size_t bytes) {
+  if (s->wfCap[i] >= bytes) return RT_OK;
+  (void)hipFree(s->wf[i]);
+  s->wf[i] = nullptr;
+  s->wfCap[i] = 0;
+  HIPCHK(hipMalloc(&s->wf[i], bytes));
+  s->wfCap[i] = bytes;
+  return RT_OK;
+}
+template <uint32_t F>
+static int render_wf(rt_scene* s, const SceneD& sd, const ParamsD& P, float* d_rgb, int32_t* d_argb, hipStream_t st) {
+  using dv::WfNode;
+  using dv::WfRay;
+  const int ncols = P.W, tilesX = (ncols + P.tw - 1) / P.tw, ntiles = tilesX * ((P.nrows + P.th - 1) / P.th);
+  const int rounds = (P.spp + P.G - 1) / P.G;
+  const int chunk = std::max(1, std::min(ntiles, (int)(RT_WF_CHUNK / (64L * rounds))));
+  const size_t slots = (size_t)chunk * rounds * 64;
+  int rc;
+  typedef rt_scene R;
+  if ((rc = wf_grow(s, R::WF_NODE0, slots * sizeof(WfNode))) || (rc = wf_grow(s, R::WF_SCOL, slots * 3 * sizeof(double))) ||
+      (rc = wf_grow(s, R::WF_TRACED, slots)) || (rc = wf_grow(s, R::WF_CNT, 16 * sizeof(int))) ||
+      (rc = wf_grow(s, R::WF_Q1, 2 * slots * sizeof(WfRay))))
+    return rc;
+  const int dof = ((F & dv::FT_DOF) && sd.dof && !((F & dv::FT_CAMX) && P.cam != 0)) ? 1 : 0;
+  for (int t0 = 0; t0 < ntiles; t0 += chunk) {
+    const int n = std::min(chunk, ntiles - t0), units = n * rounds;
+    int* cnt = (int*)s->wf[R::WF_CNT];
+    HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(int), st));
+    WfNode* node0 = (WfNode*)s->wf[R::WF_NODE0];
+    double* scol = (double*)s->wf[R::WF_SCOL];
+    uint8_t* straced = (uint8_t*)s->wf[R::WF_TRACED];
+    hipLaunchKernelGGL(dv::wf_camera_kernel<F>, dim3(units), dim3(64), dv::LDS_RENDER_BYTES, st, sd, P, t0, rounds, node0,
+                       scol, straced, (WfRay*)s->wf[R::WF_Q1], cnt + 1);
+    HIPCHK(hipGetLastError());
+    int counts[9] = {0};
+    int L = 1;
+    for (; L <= 7; ++L) {  // level L reads queue L % 2 (WF_Q0 / WF_Q1), writes the other one
+      int c = 0;
+      HIPCHK(hipMemcpyAsync(&c, cnt + L, sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (c == 0) break;
+      counts[L] = c;
+      const int qin = (L % 2) ? R::WF_Q1 : R::WF_Q0, qout = (L % 2) ? R::WF_Q0 : R::WF_Q1;
+      if ((rc = wf_grow(s, R::WF_NODE1 + L - 1, (size_t)c * sizeof(WfNode))) ||
+          (rc = wf_grow(s, qout, (size_t)2 * c * sizeof(WfRay))))
+        return rc;
+      WfNode* prev = L == 1 ? node0 : (WfNode*)s->wf[R::WF_NODE1 + L - 2];
+      hipLaunchKernelGGL(dv::wf_level_kernel<F>, dim3((unsigned)((c + 63) / 64)), dim3(64), dv::LDS_RENDER_BYTES, st, sd, P,
+                         (const WfRay*)s->wf[qin], cnt + L, (WfNode*)s->wf[R::WF_NODE1 + L - 1], prev, scol, L == 1 ? 1 : 0,
+                         (WfRay*)s->wf[qout], cnt + L + 1);
+      HIPCHK(hipGetLastError());
+    }
+    for (int l = L - 1; l >= 1; --l) {  // bottom up: a level's frames into their parents
+      WfNode* prev = l == 1 ? node0 : (WfNode*)s->wf[R::WF_NODE1 + l - 2];
+      hipLaunchKernelGGL(dv::wf_fold_kernel<F>, dim3((unsigned)((counts[l] + 255) / 256)), dim3(256), 0, st, sd,
+                         (const WfNode*)s->wf[R::WF_NODE1 + l - 1], cnt + l, 0, prev, scol);
+    }
+    hipLaunchKernelGGL(dv::wf_fold_kernel<F>, dim3((unsigned)((units * 64 + 255) / 256)), dim3(256), 0, st, sd,
+                       (const WfNode*)node0, (const int*)nullptr, units * 64, (WfNode*)nullptr, scol);
+    hipLaunchKernelGGL(dv::wf_final_kernel<F>, dim3(n), dim3(64), 0, st, P, t0, rounds, (const double*)scol,
+                       (const uint8_t*)straced, d_rgb, d_argb, dof);
+    HIPCHK(hipGetLastError());
+  }
+  return RT_OK;
+}
+static int render_wavefront(rt_scene* s, const SceneD& sd, const ParamsD& P, uint32_t flags, float* d_rgb, int32_t* d_argb,
+                            hipStream_t st) {
+  const uint32_t f = (flags & RT_RENDER_GENERIC) ? (uint32_t)dv::FT_ALL : scene_features(s->hs);
+  constexpr uint32_t C4 = dv::FT_PRIM | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX;
+  if (f == 0) return render_wf<0u>(s, sd, P, d_rgb, d_argb, st);
+  if ((f & ~C4) == 0) return render_wf<C4>(s, sd, P, d_rgb, d_argb, st);
+  return render_wf<dv::FT_ALL>(s, sd, P, d_rgb, d_argb, st);
+}
+
 // tiles: an explicit tile list (rt_render_tiles_device) -- ntiles blocks, block b renders tiles[b]
 static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, int32_t* d_argb, bool count,
                   hipStream_t st, const int32_t* tiles = nullptr, int ntiles = 0) {
   ParamsD P = P0;
   int tilesX = ((P.W + P.colStep - 1) / P.colStep + P.tw - 1) / P.tw, tilesY = (P.nrows + P.th - 1) / P.th;
   dim3 grid(dv::xcd_grid(tilesX * tilesY)), block(64);
+  if ((flags & RT_RENDER_WAVEFRONT) && !count) {
+    if (tiles) return set_error(RT_E_INVALID, "RT_RENDER_WAVEFRONT renders whole layouts, not tile lists");
+    SceneD sd = s->dev;
+    sd.fastSlab |= SCENE_NEAREST_FIRST;
+    if (sd.ntop <= 64 && !(flags & RT_RENDER_NOWAVECULL)) sd.fastSlab |= SCENE_WAVE_CULL;
+    if (flags & RT_RENDER_NOCULL) { sd.topBound = s->noCullBound; sd.fastSlab &= ~(SCENE_NEAREST_FIRST | SCENE_WAVE_CULL); }
+    if (P.colStep != 1) return set_error(RT_E_INVALID, "RT_RENDER_WAVEFRONT: not for refine passes");
+    return render_wavefront(s, sd, P, flags, d_rgb, d_argb, st);
+  }
   if (tiles) {
     P.order = const_cast<int32_t*>(tiles);
     P.tcost = nullptr;

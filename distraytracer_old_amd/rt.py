@@ -180,6 +180,7 @@ RENDER_ROWMAJOR = 2  # RT_RENDER_ROWMAJOR: row-major tile dispatch instead of th
 RENDER_NOCULL = 4  # RT_RENDER_NOCULL: no bounding-sphere culling of top-level primitives
 RENDER_SHCOMPACT = 8  # RT_RENDER_SHCOMPACT: a wave's shadow rays traced compacted (same image)
 RENDER_NOWAVECULL = 16  # RT_RENDER_NOWAVECULL: no wave-level shadow candidate test (same image)
+RENDER_WAVEFRONT = 32  # RT_RENDER_WAVEFRONT: level-synchronous shading (same image)
 
 
 def params(W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, flags=0, row_band=1) -> RenderParams:

@@ -186,6 +186,10 @@ typedef struct rt_render_params {
 /* turn off the wave-level candidate test of shadow rays against the top-level entries' bounding
    spheres (DESIGN.md §4 "Wave-level shadow cull"): same image; for A/B timing and testing */
 #define RT_RENDER_NOWAVECULL 16u
+/* level-synchronous shading (DESIGN.md §4 "Level-synchronous shading"): each generation of the shading
+   tree is one launch over a compacted ray queue, frames in HBM records, folded bottom up; same image.
+   Blocks until the frame is done (it reads each level's ray count); not with tile lists. */
+#define RT_RENDER_WAVEFRONT 32u
 
 typedef struct rt_scene rt_scene;
 

@@ -364,6 +364,31 @@ def test_more_than_64_top_level_entries(tmp_path, n_side):
     assert_exact_decisions(compare(ra, aa, ro, ao))
 
 
+@pytest.mark.parametrize("cli,W,spp", [("plnts3ColsBunnies.cli", 96, 4), ("c2clear.cli", 96, 1), ("trTrans.cli", 96, 2),
+                                       ("c3_bun69k.cli", 128, 4), ("p2_t07.cli", 96, 2), ("old_t10.cli", 96, 4),
+                                       ("t11.cli", 64, 2), ("p3_t11_sierp.cli", 64, 1), ("c4InSphere.cli", 96, 1),
+                                       ("t01.cli", 96, 1)])
+def test_wavefront_renders_identically(cli, W, spp):
+    """RT_RENDER_WAVEFRONT (level-synchronous shading: one launch per generation of the shading tree,
+    children compacted into the next level's queue, frames folded bottom up) renders the monolithic
+    kernel's image bit for bit: glass (Fresnel and simple), mirrors, DOF, fisheye, photon map,
+    instances, 1 spp -- in the scene's variant and the generic one."""
+    scenes.ensure_bun69k()
+    g = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+    ra, aa = g.render(W, W, spp=spp, seed=SEED)
+    for flags in (rt.RENDER_WAVEFRONT, rt.RENDER_WAVEFRONT | rt.RENDER_GENERIC):
+        rb, ab = g.render(W, W, spp=spp, seed=SEED, flags=flags)
+        assert np.array_equal(aa, ab), flags
+        assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32)), flags
+
+
+def test_wavefront_c4_oracle_parity():
+    """The level-synchronous path against the oracle on C4's scene (glass bunnies, mirrors, textures)."""
+    g, o, _, (ro, ao) = both("plnts3ColsBunnies.cli", 160, 160, 2, seed=0x5EED0004)
+    rg, ag = g.render(160, 160, spp=2, seed=0x5EED0004, flags=rt.RENDER_WAVEFRONT)
+    assert_exact_decisions(compare(rg, ag, ro, ao))
+
+
 def test_photon_shards_merge_to_the_full_prepass(tmp_path):
     """Multi-GPU photon pre-pass (8(e)): shards shot separately and merged in rank order give
     the single-GPU photon_list bit for bit, and the same image."""
