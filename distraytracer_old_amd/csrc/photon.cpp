@@ -199,3 +199,13 @@ void build_photon_tree(HostScene& hs, const std::vector<double>& pos, const std:
 }
 
 }  // namespace rt
+
+// Host-only: the reference's kd-tree over a photon_list (photon = list index), for tests.
+extern "C" int rt_photon_kdtree(const double* pos, int64_t n, int32_t* out) {
+  if (n < 0 || (n > 0 && (!pos || !out))) return rt::set_error(RT_E_INVALID, "rt_photon_kdtree: bad arguments");
+  if (n > INT32_MAX / 4) return rt::set_error(RT_E_INVALID, "rt_photon_kdtree: too many photons");
+  std::vector<double> p(pos, pos + 3 * n);
+  std::vector<rt::KdNodeD> kd = rt::build_java_kdtree(p);
+  std::memcpy(out, kd.data(), kd.size() * sizeof(rt::KdNodeD));
+  return RT_OK;
+}

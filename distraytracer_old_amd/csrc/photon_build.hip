@@ -197,6 +197,122 @@ static int64_t t_count(int64_t c, std::map<int64_t, int64_t>& memo) {
   return v;
 }
 
+// ---------------------------------------------------------------------------
+// The reference's kd-tree (myKD_Tree.build_tree, myLight.java:332-381; KdNodeD) on the device, level
+// by level. Every range ("segment") of a level holds its photons in the reference's current order,
+// contiguously, in segment order. One level: the segments' extents (wave-aggregated 64-bit atomic
+// min / max of order-preserving keys; mins / maxs start from +-1e20 like the Java) pick each split
+// axis; two stable radix sorts -- every photon by its coordinate on its segment's axis (+ 0.0: -0
+// ties +0 as Java's `<` does), then by segment -- are Collections.sort of every segment at once (a
+// tie keeps the previous order); the median at size / 2 becomes the node, the two sides the next
+// level's segments (a side of one photon is a leaf at once). Nodes are numbered in DFS pre-order:
+// the left child of node q is q + 1, the right one q + 1 + split.
+namespace kd {
+struct Seg {
+  int32_t start, size, node, axis;
+  int32_t lid, rid, lstart, rstart;  // the children's next-level segments (-1: none) and positions
+};
+__device__ inline uint64_t okey(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v + 0.0);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ inline double okey_inv(uint64_t k) {
+  return __builtin_bit_cast(double, (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k);
+}
+__global__ void k_iota(int32_t* __restrict__ perm, int32_t* __restrict__ segOf, int32_t n) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) { perm[i] = i; segOf[i] = 0; }
+}
+__global__ void k_ext_init(unsigned long long* __restrict__ ext, int32_t nseg) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nseg * 6) ext[i] = (i % 6) < 3 ? ~0ull : 0ull;
+}
+// 64-thread blocks: a wave whose photons are all in one segment reduces first (one atomic per value)
+__global__ void __launch_bounds__(64) k_ext(const double* __restrict__ pos, const int32_t* __restrict__ perm,
+                                            const int32_t* __restrict__ segOf, int32_t nAct, unsigned long long* __restrict__ ext) {
+  const int32_t p = blockIdx.x * 64 + threadIdx.x;
+  const bool valid = p < nAct;
+  const int32_t s = valid ? segOf[p] : -1;
+  unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0, 0, 0};
+  if (valid)
+    for (int c = 0; c < 3; ++c) mn[c] = mx[c] = okey(pos[3 * (size_t)perm[p] + c]);
+  const int32_t s0 = __shfl(s, 0);
+  if (__all(!valid || s == s0)) {
+    for (int off = 32; off >= 1; off >>= 1)
+      for (int c = 0; c < 3; ++c) {
+        const unsigned long long a = __shfl_xor(mn[c], off), b = __shfl_xor(mx[c], off);
+        mn[c] = a < mn[c] ? a : mn[c];
+        mx[c] = b > mx[c] ? b : mx[c];
+      }
+    if (threadIdx.x == 0)
+      for (int c = 0; c < 3; ++c) { atomicMin(ext + 6 * s0 + c, mn[c]); atomicMax(ext + 6 * s0 + 3 + c, mx[c]); }
+  } else if (valid) {
+    for (int c = 0; c < 3; ++c) { atomicMin(ext + 6 * s + c, mn[c]); atomicMax(ext + 6 * s + 3 + c, mx[c]); }
+  }
+}
+__global__ void k_axis(Seg* __restrict__ seg, const unsigned long long* __restrict__ ext, int32_t nseg) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nseg) return;
+  double d[3];
+  for (int c = 0; c < 3; ++c) {  // mins / maxs from +-1e20 (build_tree :343-353)
+    const double lo = fmin(1e20, okey_inv(ext[6 * i + c])), hi = fmax(-1e20, okey_inv(ext[6 * i + 3 + c]));
+    d[c] = hi - lo;
+  }
+  seg[i].axis = (d[0] >= d[1] && d[0] >= d[2]) ? 0 : (d[1] >= d[0] && d[1] >= d[2]) ? 1 : 2;
+}
+__global__ void k_keys(const double* __restrict__ pos, const int32_t* __restrict__ perm, const int32_t* __restrict__ segOf,
+                       const Seg* __restrict__ seg, int32_t nAct, uint64_t* __restrict__ key, uint64_t* __restrict__ val) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nAct) return;
+  const int32_t s = segOf[p], i = perm[p];
+  key[p] = okey(pos[3 * (size_t)i + seg[s].axis]);
+  val[p] = ((uint64_t)(uint32_t)s << 32) | (uint32_t)i;
+}
+__global__ void k_unpack(const uint64_t* __restrict__ val, int32_t nAct, uint32_t* __restrict__ skey, int32_t* __restrict__ perm) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nAct) return;
+  skey[p] = (uint32_t)(val[p] >> 32);
+  perm[p] = (int32_t)(uint32_t)val[p];
+}
+__global__ void k_seg_count(const Seg* __restrict__ seg, int32_t nseg, int32_t* __restrict__ emits, int32_t* __restrict__ elems) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nseg) return;
+  const int32_t split = seg[i].size / 2, nl = split, nr = seg[i].size - split - 1;
+  emits[i] = (nl > 1) + (nr > 1);
+  elems[i] = (nl > 1 ? nl : 0) + (nr > 1 ? nr : 0);
+}
+__global__ void k_seg_make(Seg* __restrict__ seg, int32_t nseg, const int32_t* __restrict__ perm,
+                           const int32_t* __restrict__ leafOf, const int32_t* __restrict__ sbase, const int32_t* __restrict__ pbase,
+                           KdNodeD* __restrict__ kd, Seg* __restrict__ next) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nseg) return;
+  Seg S = seg[i];
+  const int32_t split = S.size / 2, nl = split, nr = S.size - split - 1;
+  const int32_t q = S.node, ql = q + 1, qr = q + 1 + split;
+  kd[q] = KdNodeD{leafOf[perm[S.start + split]], S.axis, nl > 0 ? ql : -1, nr > 0 ? qr : -1};
+  if (nl == 1) kd[ql] = KdNodeD{leafOf[perm[S.start]], -1, -1, -1};
+  if (nr == 1) kd[qr] = KdNodeD{leafOf[perm[S.start + split + 1]], -1, -1, -1};
+  int32_t b = sbase[i], pb = pbase[i];
+  S.lid = S.rid = -1;
+  if (nl > 1) { S.lid = b; S.lstart = pb; next[b] = Seg{pb, nl, ql, 0, -1, -1, 0, 0}; ++b; pb += nl; }
+  if (nr > 1) { S.rid = b; S.rstart = pb; next[b] = Seg{pb, nr, qr, 0, -1, -1, 0, 0}; }
+  seg[i] = S;
+}
+__global__ void k_move(const Seg* __restrict__ seg, const uint32_t* __restrict__ skey, const int32_t* __restrict__ perm,
+                       int32_t nAct, int32_t* __restrict__ perm2, int32_t* __restrict__ segOf2) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nAct) return;
+  const Seg& S = seg[skey[p]];
+  const int32_t j = p - S.start, split = S.size / 2;
+  if (j < split && S.lid >= 0) { perm2[S.lstart + j] = perm[p]; segOf2[S.lstart + j] = S.lid; }
+  else if (j > split && S.rid >= 0) { perm2[S.rstart + (j - split - 1)] = perm[p]; segOf2[S.rstart + (j - split - 1)] = S.rid; }
+}
+__global__ void k_leaf_of(const int32_t* __restrict__ L0, int32_t n, int32_t* __restrict__ leafOf) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) leafOf[L0[i]] = i;
+}
+}  // namespace kd
+
 struct DevBuf {  // scratch allocations of one build, freed on every path
   std::vector<void*> p;
   template <class T>
@@ -222,8 +338,75 @@ struct DevBuf {  // scratch allocations of one build, freed on every path
 
 // Build the photon map of photon_list (pos / pwr, insertion order) on the scene's device.
 // out: device arrays owned by the scene (allocs); n > PHOTON_LEAF.
-int build_photon_tree_gpu(rt_scene* s, const double* pos_h, const double* pwr_h, int64_t n64,
-                          std::future<std::vector<KdNodeD>>& kdF) {
+// the reference's kd-tree of photon_list (device pos, list order) into kdOut, photons as leaf-order
+// indices (leafOf[list index])
+static int build_java_kdtree_gpu(const double* pos, int32_t n, const int32_t* leafOf, KdNodeD* kdOut) {
+  using namespace pb;
+  using namespace pb::kd;
+  const int TB = 256;
+  auto grid = [&](int64_t m) { return dim3((unsigned)std::max<int64_t>(1, (m + TB - 1) / TB)); };
+  DevBuf tmp;
+  int32_t *perm, *perm2, *segOf, *segOf2, *emits, *elems, *sbase, *pbase;
+  uint32_t *skey, *skey2;
+  uint64_t *key, *key2, *val, *val2;
+  unsigned long long* ext;
+  Seg *seg, *next;
+  const size_t maxSeg = (size_t)n / 2 + 2;
+  PBCHK(tmp.alloc(&perm, n)); PBCHK(tmp.alloc(&perm2, n));
+  PBCHK(tmp.alloc(&segOf, n)); PBCHK(tmp.alloc(&segOf2, n));
+  PBCHK(tmp.alloc(&skey, n)); PBCHK(tmp.alloc(&skey2, n));
+  PBCHK(tmp.alloc(&key, n)); PBCHK(tmp.alloc(&key2, n));
+  PBCHK(tmp.alloc(&val, n)); PBCHK(tmp.alloc(&val2, n));
+  PBCHK(tmp.alloc(&ext, 6 * maxSeg));
+  PBCHK(tmp.alloc(&seg, maxSeg)); PBCHK(tmp.alloc(&next, maxSeg));
+  PBCHK(tmp.alloc(&emits, maxSeg)); PBCHK(tmp.alloc(&elems, maxSeg));
+  PBCHK(tmp.alloc(&sbase, maxSeg)); PBCHK(tmp.alloc(&pbase, maxSeg));
+  size_t b1 = 0, b2 = 0, b3 = 0;
+  PBCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, key, key2, val, val2, n));
+  PBCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, skey, skey2, perm, perm2, n));
+  PBCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, b3, emits, sbase, (int)maxSeg));
+  void* cub = nullptr;
+  const size_t cb = std::max(b1, std::max(b2, b3));
+  PBCHK(tmp.alloc((char**)&cub, cb));
+  hipLaunchKernelGGL(k_iota, grid(n), dim3(TB), 0, 0, perm, segOf, n);
+  const Seg root{0, n, 0, 0, -1, -1, 0, 0};
+  PBCHK(hipMemcpy(seg, &root, sizeof(Seg), hipMemcpyHostToDevice));
+  int32_t nseg = 1, nAct = n;
+  while (nseg > 0) {
+    int segBits = 1;
+    while ((1ll << segBits) < nseg) ++segBits;
+    hipLaunchKernelGGL(k_ext_init, grid(6LL * nseg), dim3(TB), 0, 0, ext, nseg);
+    hipLaunchKernelGGL(k_ext, dim3((unsigned)((nAct + 63) / 64)), dim3(64), 0, 0, pos, perm, segOf, nAct, ext);
+    hipLaunchKernelGGL(k_axis, grid(nseg), dim3(TB), 0, 0, seg, ext, nseg);
+    hipLaunchKernelGGL(k_keys, grid(nAct), dim3(TB), 0, 0, pos, perm, segOf, seg, nAct, key, val);
+    PBCHK(hipGetLastError());
+    size_t b = cb;  // the coordinate on the segment's axis, then the segment: stable, so ties keep the order
+    PBCHK(hipcub::DeviceRadixSort::SortPairs(cub, b, key, key2, val, val2, nAct));
+    hipLaunchKernelGGL(k_unpack, grid(nAct), dim3(TB), 0, 0, val2, nAct, skey, perm);
+    b = cb;
+    PBCHK(hipcub::DeviceRadixSort::SortPairs(cub, b, skey, skey2, perm, perm2, nAct, 0, segBits));
+    hipLaunchKernelGGL(k_seg_count, grid(nseg), dim3(TB), 0, 0, seg, nseg, emits, elems);
+    b = cb;
+    PBCHK(hipcub::DeviceScan::ExclusiveSum(cub, b, emits, sbase, nseg));
+    b = cb;
+    PBCHK(hipcub::DeviceScan::ExclusiveSum(cub, b, elems, pbase, nseg));
+    hipLaunchKernelGGL(k_seg_make, grid(nseg), dim3(TB), 0, 0, seg, nseg, perm2, leafOf, sbase, pbase, kdOut, next);
+    hipLaunchKernelGGL(k_move, grid(nAct), dim3(TB), 0, 0, seg, skey2, perm2, nAct, perm, segOf);
+    PBCHK(hipGetLastError());
+    int32_t lastS[2], lastE[2];
+    PBCHK(hipMemcpy(lastS, sbase + nseg - 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+    PBCHK(hipMemcpy(lastS + 1, emits + nseg - 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+    PBCHK(hipMemcpy(lastE, pbase + nseg - 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+    PBCHK(hipMemcpy(lastE + 1, elems + nseg - 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+    nseg = lastS[0] + lastS[1];
+    nAct = lastE[0] + lastE[1];
+    std::swap(seg, next);
+  }
+  PBCHK(hipDeviceSynchronize());
+  return RT_OK;
+}
+
+int build_photon_tree_gpu(rt_scene* s, const double* pos_h, const double* pwr_h, int64_t n64) {
   using namespace pb;
   const int32_t n = (int32_t)n64;
   const int TB = 256;
@@ -323,12 +506,13 @@ int build_photon_tree_gpu(rt_scene* s, const double* pos_h, const double* pwr_h,
   hipLaunchKernelGGL(k_gather, dim3(gn), dim3(TB), 0, 0, L[0], n, pos, pwr, ppos, ppwr);
   PBCHK(hipGetLastError());
   PBCHK(hipDeviceSynchronize());
-  {  // the reference's kd-tree (built on a host thread meanwhile), photons renumbered to leaf order
-    std::vector<int32_t> leafToList(n);
-    PBCHK(hipMemcpy(leafToList.data(), L[0], sizeof(int32_t) * n, hipMemcpyDeviceToHost));
-    std::vector<KdNodeD> kd = kdF.get();
-    kd_to_leaf_order(kd, leafToList);
-    PBCHK(hipMemcpy(nodes + nnodes, kd.data(), sizeof(KdNodeD) * kd.size(), hipMemcpyHostToDevice));
+  {  // the reference's kd-tree after the BVH records, photons as leaf-order indices
+    int32_t* leafOf = nullptr;
+    PBCHK(tmp.alloc(&leafOf, n));
+    hipLaunchKernelGGL(pb::kd::k_leaf_of, dim3(gn), dim3(TB), 0, 0, L[0], n, leafOf);
+    PBCHK(hipGetLastError());
+    int rc = build_java_kdtree_gpu(pos, n, leafOf, reinterpret_cast<KdNodeD*>(nodes + nnodes));
+    if (rc) return rc;
     const int32_t off = (int32_t)nnodes;
     PBCHK(hipMemcpy(&nodes[0].padR[2], &off, sizeof(int32_t), hipMemcpyHostToDevice));
   }

@@ -1,7 +1,6 @@
 // Internal host-side declarations shared by the loader, builder and HIP launch code.
 #pragma once
 #include <cstring>
-#include <future>
 #include <string>
 #include <vector>
 
@@ -63,9 +62,8 @@ void kd_to_leaf_order(std::vector<KdNodeD>& kd, const std::vector<int32_t>& leaf
 struct rt_scene;
 namespace rt {
 // photon_build.hip: the same structure built on the scene's device (n > PHOTON_LEAF)
-// kd: the reference's kd-tree over photon_list indices (build_java_kdtree), stored after the BVH
-int build_photon_tree_gpu(rt_scene* s, const double* pos, const double* pwr, int64_t n,
-                          std::future<std::vector<KdNodeD>>& kd);
+// (with the reference's kd-tree after the BVH records, built on the device too)
+int build_photon_tree_gpu(rt_scene* s, const double* pos, const double* pwr, int64_t n);
 }  // namespace rt
 
 struct rt_scene {

@@ -1161,10 +1161,7 @@ static int set_photon_map(rt_scene* s, std::vector<double>& pos, std::vector<dou
   const char* mode = std::getenv("DISTRAYTRACER_PHOTON_BUILD");
   if (n > PHOTON_LEAF && !(mode && std::string(mode) == "host")) {
     HIPCHK(hipSetDevice(s->device));
-    // the reference's kd-tree on a host thread while the device builds the BVH
-    std::future<std::vector<KdNodeD>> kd = std::async(std::launch::async, [&pos] { return build_java_kdtree(pos); });
-    int rc = build_photon_tree_gpu(s, pos.data(), pwr.data(), n, kd);
-    if (kd.valid()) kd.wait();  // an early error return left it running: it reads pos
+    int rc = build_photon_tree_gpu(s, pos.data(), pwr.data(), n);
     h.photonListPos.swap(pos);
     h.photonListPwr.swap(pwr);
     return rc;
@@ -1211,6 +1208,19 @@ extern "C" int rt_photons_set(rt_scene* s, const double* pos, const double* pwr,
   std::vector<double> p(pos, pos + 3 * n), w(pwr, pwr + 3 * n);
   s->photonsUploaded = false;
   return set_photon_map(s, p, w);
+}
+
+extern "C" int rt_scene_photon_kdtree(const rt_scene* s, int32_t* out, int64_t n) {
+  if (!s || n < 0 || (n > 0 && !out)) return set_error(RT_E_INVALID, "rt_scene_photon_kdtree: bad arguments");
+  if (!s->photonsUploaded) return set_error(RT_E_INVALID, "rt_scene_photon_kdtree: no photon map");
+  n = std::min<int64_t>(n, s->hs.nphoton);
+  if (n == 0) return RT_OK;
+  HIPCHK(hipSetDevice(s->device));
+  int32_t off = 0;
+  HIPCHK(hipMemcpy(&off, &s->dev.pnode[s->dev.photonRoot].padR[2], sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (off <= 0) return set_error(RT_E_INVALID, "rt_scene_photon_kdtree: the photon map has no kd-tree");
+  HIPCHK(hipMemcpy(out, reinterpret_cast<const KdNodeD*>(s->dev.pnode + off), sizeof(KdNodeD) * n, hipMemcpyDeviceToHost));
+  return RT_OK;
 }
 
 extern "C" int rt_scene_photon_map(const rt_scene* s, void* nodes, int64_t node_cap, double* ppos, double* ppwr,

@@ -840,10 +840,25 @@ static constexpr bool PACKET = RT_PACKET != 0;  // render kernel: packet travers
 #endif
 static constexpr bool STASH_SHADE = PACKET && RT_STASH_SHADE != 0 && PK_LDS >= SL_N;
 // PK: packet traversal of the BVHs (render kernel; the lanes of a wave are coherent)
+// experiment (default off): when at least RT_LANE_DIV lanes' rays point away from the wave's first
+// ray (cosine below RT_LANE_DIV_COS), the BVHs are traversed lane by lane (accel_closest: the
+// reference order, per-lane stacks) instead of as one packet walking the union of the lanes' paths
+#ifndef RT_LANE_DIV
+#define RT_LANE_DIV 0
+#endif
+#ifndef RT_LANE_DIV_COS
+#define RT_LANE_DIV_COS 0.9
+#endif
 template <bool CNT, uint32_t F, bool PK = false>
 DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
   PROF_T0(t_all);
   Best best = miss();
+  bool lanes = false;
+  if constexpr (PK && RT_LANE_DIV > 0) {
+    const int f = (int)__builtin_ctzll(__ballot(1));
+    const double c = w.d.x * rdl(w.d.x, f) + w.d.y * rdl(w.d.y, f) + w.d.z * rdl(w.d.z, f);
+    lanes = __popcll(__ballot(!(c >= RT_LANE_DIV_COS))) >= RT_LANE_DIV;
+  }
   for (int i = 0; i < S.ntop; ++i) {
     TopD tp = PK ? sload_top(S.top + i) : S.top[i];
     if (CNT) ct.c[C_TOP]++;
@@ -872,7 +887,9 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       w.moved = false;
       double local = DMAX;
       PROF_T0(t_acc);
-      if (PK && NEAREST_FIRST && (F & (FT_PHOTON | (RT_NF_TRANS ? 0 : FT_TRANS))) == 0 && (S.fastSlab & SCENE_NEAREST_FIRST) &&
+      if (RT_LANE_DIV > 0 && lanes)
+        accel_closest<CNT, F, false>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);
+      else if (PK && NEAREST_FIRST && (F & (FT_PHOTON | (RT_NF_TRANS ? 0 : FT_TRANS))) == 0 && (S.fastSlab & SCENE_NEAREST_FIRST) &&
           (A.flags & ACCEL_NEAREST) &&
           !__ballot(!(w.stable && ri.fast)))
         accel_closest_nf<CNT, F>(S, A, o, d, ri, w, k, HitCtx{i, -1, 0}, best, local, ct);

@@ -47,7 +47,8 @@ EXPORTS = ["rt_abi_version", "rt_build_id", "rt_last_error", "rt_device_count", 
            "rt_scene_photon_map", "rt_photons_shoot",
            "rt_photons_set",
            "rt_png_name", "rt_scene_save_name", "rt_math_eval", "rt_tile_layout", "rt_tile_costs",
-           "rt_render_tiles_device", "rt_render_tiles_count", "rt_photon_gather"]
+           "rt_render_tiles_device", "rt_render_tiles_count", "rt_photon_gather",
+           "rt_photon_kdtree", "rt_scene_photon_kdtree"]
 
 _lib = None
 
@@ -110,6 +111,8 @@ def lib():
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.rt_render_tiles_count.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int,
                                             ctypes.c_void_p]
+        L.rt_photon_kdtree.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+        L.rt_scene_photon_kdtree.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         L.rt_photon_gather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         L.rt_math_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
         L.rt_png_name.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
@@ -147,6 +150,15 @@ def math_eval(x, device: int = 0) -> np.ndarray:
     x = np.ascontiguousarray(x, dtype=np.float64)
     out = np.zeros((len(x), 4), dtype=np.float64)
     _check(lib().rt_math_eval(x.ctypes.data, out.ctypes.data, len(x), device), "rt_math_eval")
+    return out
+
+
+def photon_kdtree(pos) -> np.ndarray:
+    """The reference's kd-tree over a photon_list (host-only, rt_photon_kdtree): int32 [n, 4] =
+    (photon list index, axis, left, right) per node, DFS pre-order."""
+    pos = np.ascontiguousarray(pos, dtype=np.float64).reshape(-1, 3)
+    out = np.zeros((len(pos), 4), dtype=np.int32)
+    _check(lib().rt_photon_kdtree(pos.ctypes.data, len(pos), out.ctypes.data), "rt_photon_kdtree")
     return out
 
 
@@ -325,6 +337,13 @@ class Scene:
         t = np.ascontiguousarray(tiles, dtype=np.int32)
         _check(lib().rt_render_tiles_device(self._h, ctypes.byref(p), t.ctypes.data, len(t), ctypes.c_void_p(rgb_ptr),
                                             ctypes.c_void_p(argb_ptr), ctypes.c_void_p(stream)), "rt_render_tiles_device")
+
+    def photon_kdtree(self) -> np.ndarray:
+        """The device's copy of the reference's kd-tree: int32 [n, 4] (leaf-order photon, axis, left, right)."""
+        n = self.info()["photons"]
+        out = np.zeros((n, 4), dtype=np.int32)
+        _check(lib().rt_scene_photon_kdtree(self._h, out.ctypes.data, n), "rt_scene_photon_kdtree")
+        return out
 
     def photon_gather(self, pts) -> np.ndarray:
         """The render kernel's photon gather at points pts [n, 3] -> irradiance [n, 3] (rt_photon_gather)."""

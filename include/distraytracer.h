@@ -305,6 +305,13 @@ int rt_math_eval(const double* x, double* out, int64_t n, int device);
 /* Diagnostics: the render kernel's photon gather (getIrradianceFromPhtnTree, myObjShader.java:441-458)
    at points pts[3*i..3*i+2] into out[3*i..3*i+2] (host buffers); needs the scene's photon map. */
 int rt_photon_gather(rt_scene* scene, const double* pts, double* out, int64_t n);
+/* Host-only: the reference's photon kd-tree (myKD_Tree.build_tree, myLight.java:332-381) over a
+   photon_list pos[3*n] (insertion order), as the device's tie replay uses it: out[4*i..4*i+3] =
+   {photon (list index), split axis (-1: leaf), left, right} of node i, DFS pre-order, root 0. */
+int rt_photon_kdtree(const double* pos, int64_t n, int32_t* out);
+/* The scene's device copy of that kd-tree (n = photon count): out[4*i..4*i+3] = {photon as its index in
+   the photon map's leaf-ordered arrays (rt_scene_photon_map ppos / ppwr), axis, left, right}. */
+int rt_scene_photon_kdtree(const rt_scene* scene, int32_t* out, int64_t n);
 
 #ifdef __cplusplus
 }

@@ -86,3 +86,26 @@ def test_render_with_tied_neighbourhoods_matches_oracle(tmp_path, k):
     rg, ag = g.render(64, 64, spp=1, seed=7)
     ro, ao, _ = o.render(64, 64, spp=1, seed=7)
     assert_exact_decisions(compare(rg, ag, ro, ao))
+
+
+@pytest.mark.parametrize("n", [25, 187, 60000, 262147])
+def test_device_kdtree_is_the_references(tmp_path, monkeypatch, n):
+    """The kd-tree the tie replay walks, built on the device (photon_build.hip: per-level stable radix
+    sorts), is the reference's build_tree node for node: the host restatement (rt_photon_kdtree,
+    itself pinned against tests/test_knn_ties.py's Python build_tree) with every photon identified by
+    its position and power in the photon map's leaf order. Duplicated lattice points and signed
+    zeros make the stable-sort ties decisive; n = 25 is the smallest map built on the device."""
+    (tmp_path / "t.cli").write_text("fov 60\nbackground 0 0 0\npoint_light 0 5 0 1 1 1\ndiffuse_photons 100 8 10\n"
+                                    "diffuse .5 .5 .5 0 0 0\nsphere 1 0 0 -5\n")
+    rng = np.random.default_rng(n)
+    pos = rng.integers(-6, 7, size=(n, 3)).astype(np.float64) * 0.5
+    pos[rng.random((n, 3)) < 0.1] = -0.0
+    pwr = rng.random((n, 3))
+    g = rt.Scene.load_cli("t.cli", scene_dir=tmp_path, textures={})
+    g.set_photons(pos, pwr)
+    dev = g.photon_kdtree()
+    _, ppos, ppwr, _ = g.photon_map()
+    host = rt.photon_kdtree(pos)
+    assert np.array_equal(dev[:, 1:], host[:, 1:])
+    assert np.array_equal(ppos[dev[:, 0]], pos[host[:, 0]])
+    assert np.array_equal(ppwr[dev[:, 0]], pwr[host[:, 0]])

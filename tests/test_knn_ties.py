@@ -126,3 +126,34 @@ def test_knn_ties_follow_java_priority_queue(tmp_path, k, seed):
         assert [d for d, _ in exp] == d2.tolist()
         ties += len(set(d for d, _ in exp)) < len(exp)
     assert ties == len(queries)  # every neighbourhood holds equally distant photons
+
+
+def _flatten(node, out):  # the Python build_tree's nodes in DFS pre-order: (photon id, axis, left, right)
+    me = len(out)
+    (_, pid), ax, left, right = node
+    out.append([pid, ax, -1, -1])
+    if left is not None:
+        out[me][2] = len(out)
+        _flatten(left, out)
+    if right is not None:
+        out[me][3] = len(out)
+        _flatten(right, out)
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_product_kdtree_is_the_references(seed):
+    """The product's copy of myKD_Tree.build_tree (csrc/photon.cpp, the structure the device's tie
+    replay walks; host-only rt_photon_kdtree) equals the independent Python restatement node for
+    node -- on the duplicated lattice (every stable-sort tie decided by the previous order) and on
+    random photons large enough for the parallel subtree builds and the merge sort."""
+    from distraytracer_old_amd import rt
+
+    pos, _ = _lattice(seed)
+    rng = np.random.default_rng(seed)
+    big = np.concatenate([rng.random((9000, 3)), np.round(rng.random((3000, 3)) * 8) / 8])  # ties too
+    big[rng.random(len(big)) < 0.05, 1] = -0.0
+    for p in (pos, big):
+        exp = np.array(_flatten(build([(tuple(q), i) for i, q in enumerate(p.tolist())]), []), dtype=np.int32)
+        got = rt.photon_kdtree(p)
+        assert np.array_equal(got, exp)

@@ -29,8 +29,8 @@ order = np.argsort(-c, kind="stable")
 print("top tiles (us, tile, first pixel (row, col), counters):")
 for t in order[:TOP]:
     st = s.render_tiles_count(p, np.array([t], dtype=np.int32))
-    keep = {k: v for k, v in st.items() if v and not k.startswith("w_")}
+    keep = {k: v for k, v in st.items() if v}
     print(f"  {c[t]:9.1f} tile {t} px ({(t // tx) * th}, {(t % tx) * tw}) {keep}", flush=True)
 med = order[len(order) // 2]
 st = s.render_tiles_count(p, np.array([med], dtype=np.int32))
-print(f"  median tile {med} ({c[med]:.1f} us):", {k: v for k, v in st.items() if v and not k.startswith("w_")})
+print(f"  median tile {med} ({c[med]:.1f} us):", {k: v for k, v in st.items() if v})

@@ -80,6 +80,12 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "ant": ["RT_AN_TRANS=1"],                  # nearest-first any-hit order there
     "nftant": ["RT_NF_TRANS=1", "RT_AN_TRANS=1"],
     "nfan0": ["RT_NEAREST_FIRST=0", "RT_ANY_NEAR=0"],
+    "ld8": ["RT_LANE_DIV=8"],                  # divergent waves: per-lane BVH traversal (closest hit)
+    "ld16": ["RT_LANE_DIV=16"],
+    "ld32": ["RT_LANE_DIV=32"],
+    "ld16c99": ["RT_LANE_DIV=16", "RT_LANE_DIV_COS=0.99"],
+    "wf5": ["RT_WF_WAVES=5"],                  # level-synchronous kernels at 5 / 3 waves per SIMD
+    "wf3": ["RT_WF_WAVES=3"],
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
