@@ -628,7 +628,7 @@ static int render_wf(rt_scene* s, const SceneD& sd, const ParamsD& P, float* d_r
     double* scol = (double*)s->wf[R::WF_SCOL];
     uint8_t* straced = (uint8_t*)s->wf[R::WF_TRACED];
     hipLaunchKernelGGL(dv::wf_camera_kernel<F>, dim3(units), dim3(64), dv::LDS_RENDER_BYTES, st, sd, P, t0, rounds, node0,
-                       scol, straced, (WfRay*)s->wf[R::WF_Q1], cnt + 1);
+                       scol, straced, (WfRay*)s->wf[R::WF_Q1], cnt + 1, (int32_t)(2 * (size_t)units * 64));
     HIPCHK(hipGetLastError());
     int counts[9] = {0};
     int L = 1;
@@ -637,24 +637,28 @@ static int render_wf(rt_scene* s, const SceneD& sd, const ParamsD& P, float* d_r
       HIPCHK(hipMemcpyAsync(&c, cnt + L, sizeof(int), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       if (c == 0) break;
+      if (c > (L == 1 ? 2 * units * 64 : 2 * counts[L - 1]))
+        return set_error(RT_E_HIP, "RT_RENDER_WAVEFRONT: a ray queue overflowed");
       counts[L] = c;
       const int qin = (L % 2) ? R::WF_Q1 : R::WF_Q0, qout = (L % 2) ? R::WF_Q0 : R::WF_Q1;
       if ((rc = wf_grow(s, R::WF_NODE1 + L - 1, (size_t)c * sizeof(WfNode))) ||
           (rc = wf_grow(s, qout, (size_t)2 * c * sizeof(WfRay))))
         return rc;
       WfNode* prev = L == 1 ? node0 : (WfNode*)s->wf[R::WF_NODE1 + L - 2];
+      const int32_t nPrev = L == 1 ? units * 64 : counts[L - 1];
       hipLaunchKernelGGL(dv::wf_level_kernel<F>, dim3((unsigned)((c + 63) / 64)), dim3(64), dv::LDS_RENDER_BYTES, st, sd, P,
-                         (const WfRay*)s->wf[qin], cnt + L, (WfNode*)s->wf[R::WF_NODE1 + L - 1], prev, scol, L == 1 ? 1 : 0,
-                         (WfRay*)s->wf[qout], cnt + L + 1);
+                         (const WfRay*)s->wf[qin], cnt + L, (WfNode*)s->wf[R::WF_NODE1 + L - 1], prev, nPrev,
+                         (WfRay*)s->wf[qout], cnt + L + 1, 2 * c);
       HIPCHK(hipGetLastError());
     }
     for (int l = L - 1; l >= 1; --l) {  // bottom up: a level's frames into their parents
       WfNode* prev = l == 1 ? node0 : (WfNode*)s->wf[R::WF_NODE1 + l - 2];
+      const int32_t nPrev = l == 1 ? units * 64 : counts[l - 1];
       hipLaunchKernelGGL(dv::wf_fold_kernel<F>, dim3((unsigned)((counts[l] + 255) / 256)), dim3(256), 0, st, sd,
-                         (const WfNode*)s->wf[R::WF_NODE1 + l - 1], cnt + l, 0, prev, scol);
+                         (const WfNode*)s->wf[R::WF_NODE1 + l - 1], cnt + l, 0, prev, nPrev, scol);
     }
     hipLaunchKernelGGL(dv::wf_fold_kernel<F>, dim3((unsigned)((units * 64 + 255) / 256)), dim3(256), 0, st, sd,
-                       (const WfNode*)node0, (const int*)nullptr, units * 64, (WfNode*)nullptr, scol);
+                       (const WfNode*)node0, (const int*)nullptr, units * 64, (WfNode*)nullptr, 0, scol);
     hipLaunchKernelGGL(dv::wf_final_kernel<F>, dim3(n), dim3(64), 0, st, P, t0, rounds, (const double*)scol,
                        (const uint8_t*)straced, d_rgb, d_argb, dof);
     HIPCHK(hipGetLastError());

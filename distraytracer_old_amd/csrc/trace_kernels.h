@@ -1631,9 +1631,9 @@ DEVI V irradiance_heap(const SceneD& S, V p, Counters& ct) {
 
 // Photon scan: f(d2, photon) for every photon with d2 < R2 (photon BVH, depth first,
 // children pruned by box distance^2 >= R2; see box_d2). Order is irrelevant to its users.
-template <bool CNT, bool PWR, class Fn>
+template <bool CNT, bool PWR, int NL = STK_LDS, class Fn>
 DEVI void photon_scan(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f) {
-  NStack st;  // the ray-traversal stack is idle during shading
+  NStackT<NL> st;  // the ray-traversal stack is idle during shading
   int sp = 0;
   int32_t N = S.photonRoot;
   while (true) {
@@ -1783,9 +1783,17 @@ DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters
     act = uni64(fM[sp]);
   }
 }
+// experiment (default off): a wave whose query points are far apart (RT_KNN_DIV or more lanes farther
+// than 2 start radii from the first lane's) scans lane by lane -- each lane its own neighbourhood,
+// stacks in scratch (the pkT levels hold the counting histogram) -- instead of one packet walking the
+// union of 64 neighbourhoods
+#ifndef RT_KNN_DIV
+#define RT_KNN_DIV 0
+#endif
 template <bool CNT, bool PWR = false, class Fn>
-DEVI void photon_scan_any(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f) {
-  if (PACKET) photon_scan_pk<CNT, PWR>(S, pos, R2, ct, f);
+DEVI void photon_scan_any(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f, bool lanewise = false) {
+  if (PACKET && RT_KNN_DIV > 0 && lanewise) photon_scan<CNT, PWR, 0>(S, pos, R2, ct, f);
+  else if (PACKET) photon_scan_pk<CNT, PWR>(S, pos, R2, ct, f);
   else photon_scan<CNT, PWR>(S, pos, R2, ct, f);
 }
 
@@ -1833,7 +1841,7 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // whose counts may have carried between the halves (the caller repeats the pass with u32).
 template <bool CNT, int NB, bool P16>
 DEVI void knn_hist_pass(const SceneD& S, const double* pos, double lo, double hi, int K, Counters& ct,
-                        uint32_t& total, int& kb, uint32_t& cPrev, uint32_t& cAt, bool& ovf) {
+                        uint32_t& total, int& kb, uint32_t& cPrev, uint32_t& cAt, bool& ovf, bool lw = false) {
   constexpr int NW = P16 ? NB / 2 : NB;  // LDS words per lane
   static_assert(NW * 64 * 4 <= PK_LDS * 64 * 8, "histogram fits the pkT levels");
   lds_u32* hist = (lds_u32*)pkT() + __lane_id();
@@ -1860,13 +1868,13 @@ DEVI void knn_hist_pass(const SceneD& S, const double* pos, double lo, double hi
       // j0 <= NB: d2 < hi; a j0 of NB (rounding) can only mean j = NB - 1, as the min keeps
       const int j0 = (int)fmax((d2 - lob) * inv, 0.0);
       bump(min(j0 + ((d2 < lo + (j0 + 1) * w) ? 0 : 1), NB - 1));  // e[j0] as below
-    });
+    }, lw);
   } else {  // some lane's window is too narrow for the bias: walk the edges from 0
     photon_scan_any<CNT>(S, pos, hi, ct, [&](double d2, int, V) {
       int j = 0;
       while (j < NB - 1 && !(d2 < lo + (j + 1) * w)) ++j;
       bump(j);
-    });
+    }, lw);
   }
   ovf = P16 && tot > (uint32_t)S.knnU16Max;
   for (int q = 0; q < NW; ++q) {
@@ -2027,6 +2035,13 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
       N = nxt;
     }
   }
+  bool lw = false;  // RT_KNN_DIV experiment: scan lane by lane
+  if constexpr (PACKET && RT_KNN_DIV > 0) {
+    const int f = (int)__builtin_ctzll(__ballot(1));
+    const double fx = rdl(pos[0], f), fy = rdl(pos[1], f), fz = rdl(pos[2], f), r2 = rdl(R2dens, f);
+    const double dx = pos[0] - fx, dy = pos[1] - fy, dz = pos[2] - fz;
+    lw = __popcll(__ballot(!(dx * dx + dy * dy + dz * dz <= 4 * r2))) >= RT_KNN_DIV;
+  }
   // --- bracket the k-th d^2: window [lo, hi), `below` photons under lo
   PROF_CNT(R_KNN_NCALL);
   double lo = 0, hi = R2dens;
@@ -2042,12 +2057,12 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
     int ne = NE;  // this lane's edges in this pass: e[k] = lo + (k + 1) w, w = (hi - lo) / ne
     if constexpr (KNN_LDS_HIST) {
       bool ovf = false;
-      knn_hist_pass<CNT, KNN_HB, KNN_H16>(S, pos, lo, hi, K, ct, total, kb, cPrev, cAt, ovf);
+      knn_hist_pass<CNT, KNN_HB, KNN_H16>(S, pos, lo, hi, K, ct, total, kb, cPrev, cAt, ovf, lw);
       ne = KNN_HB;
       if (KNN_H16 && __ballot(ovf)) {  // > 65535 photons below hi: this pass again with u32 buckets
         if (ovf) {
           total = cPrev = cAt = 0; kb = -1;
-          knn_hist_pass<CNT, NE, false>(S, pos, lo, hi, K, ct, total, kb, cPrev, cAt, ovf);
+          knn_hist_pass<CNT, NE, false>(S, pos, lo, hi, K, ct, total, kb, cPrev, cAt, ovf, lw);
           ne = NE;
         }
       }
@@ -2122,7 +2137,7 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
         if (m < KNN_SHELL) { ld[m * 64] = d2; li[m * 64] = i; }
         m++;
       }
-    });
+    }, lw);
 #pragma unroll
     for (int k = 0; k < KNN_SHELL; ++k)
       if (k < m) shell_insert(ld[k * 64], li[k * 64]);
@@ -2139,8 +2154,8 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
     });
   }
   // a tie across the k-th position: window photons `need` and `need + 1` (1-based) at the same
-  // distance (or more window photons than the sorted shell holds: all at one distance). Which of
-  // them the reference keeps is its kd-tree order and heap layout: such a lane replays find_near.
+  // distance. Which of them the reference keeps is its kd-tree order and heap layout: such a lane
+  // replays find_near.
   bool tie = false;
   if (!all) {
     const int need = K - below;
@@ -2156,7 +2171,9 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
       if (k == need - 1) dLast = sd[k];
       if (k == need) dNext = sd[k];
     }
-    tie = need >= 1 && need < m && (m > KNN_SHELL || dLast == dNext);
+    // (a window of more photons than the shell holds -- only photons at one distance end the bracket
+    // that way -- is replayed whether or not the tie straddles: the shell kept only its first ones)
+    tie = need >= 1 && (m > KNN_SHELL || (need < m && dLast == dNext));
   }
   PROF_ADD(t_kf, R_KNN_FINAL);
   V out = mk(0, 0, 0);

@@ -14,12 +14,14 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from distraytracer_old_amd import multigpu, rt, scenes  # noqa: E402
 
-args = [a for a in sys.argv[1:] if not a.startswith("--")]
-TILES = "--tiles" in sys.argv
+argv = sys.argv[1:]
 WORLDS = [2, 4, 8]
-if "--worlds" in sys.argv:
-    WORLDS = [int(x) for x in sys.argv[sys.argv.index("--worlds") + 1].split(",")]
-    args = [a for a in args if a != sys.argv[sys.argv.index("--worlds") + 1]]
+if "--worlds" in argv:
+    i = argv.index("--worlds")
+    WORLDS = [int(x) for x in argv[i + 1].split(",")]
+    del argv[i:i + 2]
+TILES = "--tiles" in argv
+args = [a for a in argv if not a.startswith("--")]
 BANDS = [int(x) for x in args[0].split(",")] if args else [multigpu.BAND]
 CFG = args[1] if len(args) > 1 else "C3"
 ORDERS = ((0, "schedule"), (rt.RENDER_ROWMAJOR, "row-major")) if not args and not TILES else ((0, "schedule"),)

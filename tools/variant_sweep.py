@@ -84,6 +84,9 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "ld16": ["RT_LANE_DIV=16"],
     "ld32": ["RT_LANE_DIV=32"],
     "ld16c99": ["RT_LANE_DIV=16", "RT_LANE_DIV_COS=0.99"],
+    "kd8": ["RT_KNN_DIV=8"],                   # divergent query points: per-lane photon scans
+    "kd16": ["RT_KNN_DIV=16"],
+    "kd32": ["RT_KNN_DIV=32"],
     "wf5": ["RT_WF_WAVES=5"],                  # level-synchronous kernels at 5 / 3 waves per SIMD
     "wf3": ["RT_WF_WAVES=3"],
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
