@@ -611,7 +611,9 @@ static int render_wf(rt_scene* s, const SceneD& sd, const ParamsD& P, float* d_r
   using dv::WfRay;
   const int ncols = P.W, tilesX = (ncols + P.tw - 1) / P.tw, ntiles = tilesX * ((P.nrows + P.th - 1) / P.th);
   const int rounds = (P.spp + P.G - 1) / P.G;
-  const int chunk = std::max(1, std::min(ntiles, (int)(RT_WF_CHUNK / (64L * rounds))));
+  long chunkSamples = RT_WF_CHUNK;
+  if (const char* e = std::getenv("DISTRAYTRACER_WF_CHUNK")) chunkSamples = std::max(64L, std::atol(e));  // testing knob
+  const int chunk = std::max(1, std::min(ntiles, (int)(chunkSamples / (64L * rounds))));
   const size_t slots = (size_t)chunk * rounds * 64;
   int rc;
   typedef rt_scene R;

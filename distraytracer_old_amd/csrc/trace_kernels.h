@@ -857,7 +857,8 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
   if constexpr (PK && RT_LANE_DIV > 0) {
     const int f = (int)__builtin_ctzll(__ballot(1));
     const double c = w.d.x * rdl(w.d.x, f) + w.d.y * rdl(w.d.y, f) + w.d.z * rdl(w.d.z, f);
-    lanes = __popcll(__ballot(!(c >= RT_LANE_DIV_COS))) >= RT_LANE_DIV;
+    const int nfar = __popcll(__ballot(!(c >= RT_LANE_DIV_COS))), nact = __popcll(__ballot(1));
+    lanes = RT_LANE_DIV == 1 ? (nfar >= 2 && 2 * nfar >= nact) : nfar >= RT_LANE_DIV;
   }
   for (int i = 0; i < S.ntop; ++i) {
     TopD tp = PK ? sload_top(S.top + i) : S.top[i];
@@ -2040,7 +2041,9 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
     const int f = (int)__builtin_ctzll(__ballot(1));
     const double fx = rdl(pos[0], f), fy = rdl(pos[1], f), fz = rdl(pos[2], f), r2 = rdl(R2dens, f);
     const double dx = pos[0] - fx, dy = pos[1] - fy, dz = pos[2] - fz;
-    lw = __popcll(__ballot(!(dx * dx + dy * dy + dz * dz <= 4 * r2))) >= RT_KNN_DIV;
+    // RT_KNN_DIV = 1: half of the lanes in this call (at least two) are far; >= 2: at least that many
+    const int nfar = __popcll(__ballot(!(dx * dx + dy * dy + dz * dz <= 4 * r2))), nact = __popcll(__ballot(1));
+    lw = RT_KNN_DIV == 1 ? (nfar >= 2 && 2 * nfar >= nact) : nfar >= RT_KNN_DIV;
   }
   // --- bracket the k-th d^2: window [lo, hi), `below` photons under lo
   PROF_CNT(R_KNN_NCALL);

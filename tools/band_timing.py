@@ -20,11 +20,16 @@ if "--worlds" in argv:
     i = argv.index("--worlds")
     WORLDS = [int(x) for x in argv[i + 1].split(",")]
     del argv[i:i + 2]
+FLAGS = 0
+if "--flags" in argv:
+    i = argv.index("--flags")
+    FLAGS = int(argv[i + 1])
+    del argv[i:i + 2]
 TILES = "--tiles" in argv
 args = [a for a in argv if not a.startswith("--")]
 BANDS = [int(x) for x in args[0].split(",")] if args else [multigpu.BAND]
 CFG = args[1] if len(args) > 1 else "C3"
-ORDERS = ((0, "schedule"), (rt.RENDER_ROWMAJOR, "row-major")) if not args and not TILES else ((0, "schedule"),)
+ORDERS = ((0, "schedule"), (rt.RENDER_ROWMAJOR, "row-major")) if not args and not TILES else ((FLAGS, "schedule"),)
 cli, W, H, spp, seed = scenes.CONFIGS[CFG]
 scenes.ensure_bun69k()
 s = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
@@ -52,7 +57,7 @@ for flags, name in ORDERS:
     full = s.time_render(W, H, spp=spp, seed=seed, iters=5, flags=flags)
     print(CFG, name, "full %.3f ms" % full, flush=True)
     if TILES:
-        p = rt.params(W, H, spp=spp, seed=seed)
+        p = rt.params(W, H, spp=spp, seed=seed, flags=flags)
         costs = s.tile_costs(p)
         for world in WORLDS:
             ts = [time_tiles(p, t) for t in multigpu.balanced_tiles(costs, world)]

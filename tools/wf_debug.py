@@ -10,11 +10,15 @@ from distraytracer_old_amd import rt, scenes  # noqa: E402
 
 cli = sys.argv[1] if len(sys.argv) > 1 else "plnts3ColsBunnies.cli"
 W = int(sys.argv[2]) if len(sys.argv) > 2 else 96
+SPPS = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 4]
+MODES = sys.argv[4].split(",") if len(sys.argv) > 4 else ["default", "nowavecull", "generic", "nocull"]
 scenes.ensure_bun69k()
 g = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
-for spp in (1, 4):
+for spp in SPPS:
     for extra, name in ((0, "default"), (rt.RENDER_NOWAVECULL, "nowavecull"), (rt.RENDER_GENERIC, "generic"),
                         (rt.RENDER_NOCULL, "nocull")):
+        if name not in MODES:
+            continue
         ra, aa = g.render(W, W, spp=spp, seed=0x5EED0001, flags=extra)
         rb, ab = g.render(W, W, spp=spp, seed=0x5EED0001, flags=extra | rt.RENDER_WAVEFRONT)
         d = np.abs(ra.astype(np.float64) - rb).max(-1)
