@@ -1784,12 +1784,21 @@ DEVI void photon_scan_pk(const SceneD& S, const double* pos, double R2, Counters
     act = uni64(fM[sp]);
   }
 }
-// experiment (default off): a wave whose query points are far apart (RT_KNN_DIV or more lanes farther
-// than 2 start radii from the first lane's) scans lane by lane -- each lane its own neighbourhood,
-// stacks in scratch (the pkT levels hold the counting histogram) -- instead of one packet walking the
-// union of 64 neighbourhoods
+// Divergent gathers scan lane by lane: when at least half of the lanes of a gather call (and at least
+// two) lie farther than 2 start radii from the first lane's point -- the lanes of a pixel seen through
+// the glass sphere, whose refracted samples spread over the floor -- each lane walks its own
+// neighbourhood (photon_scan, stacks in scratch: the pkT levels hold the counting histogram) instead of
+// one packet walking the union of all of them (those calls ran with ~6 lanes per wave step). Same
+// photons in the same order per lane: the image is unchanged. C5 (t11): frame 195.2 -> 196.2 ms, but
+// its slowest waves 47 -> 37 ms, the 8-GPU split's tail (profiles/r04f_*). RT_KNN_DIV = 0: packets only.
 #ifndef RT_KNN_DIV
-#define RT_KNN_DIV 0
+#define RT_KNN_DIV 1
+#endif
+#ifndef RT_KNN_DIV_FRAC
+#define RT_KNN_DIV_FRAC 2
+#endif
+#ifndef RT_KNN_DIV_R
+#define RT_KNN_DIV_R 2.0
 #endif
 template <bool CNT, bool PWR = false, class Fn>
 DEVI void photon_scan_any(const SceneD& S, const double* pos, double R2, Counters& ct, Fn&& f, bool lanewise = false) {
@@ -2041,9 +2050,11 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
     const int f = (int)__builtin_ctzll(__ballot(1));
     const double fx = rdl(pos[0], f), fy = rdl(pos[1], f), fz = rdl(pos[2], f), r2 = rdl(R2dens, f);
     const double dx = pos[0] - fx, dy = pos[1] - fy, dz = pos[2] - fz;
-    // RT_KNN_DIV = 1: half of the lanes in this call (at least two) are far; >= 2: at least that many
-    const int nfar = __popcll(__ballot(!(dx * dx + dy * dy + dz * dz <= 4 * r2))), nact = __popcll(__ballot(1));
-    lw = RT_KNN_DIV == 1 ? (nfar >= 2 && 2 * nfar >= nact) : nfar >= RT_KNN_DIV;
+    // RT_KNN_DIV = 1: 1 / RT_KNN_DIV_FRAC of the lanes in this call (at least two) are farther than
+    // RT_KNN_DIV_R start radii; >= 2: at least that many lanes are
+    const int nfar = __popcll(__ballot(!(dx * dx + dy * dy + dz * dz <= (RT_KNN_DIV_R * RT_KNN_DIV_R) * r2)));
+    const int nact = __popcll(__ballot(1));
+    lw = RT_KNN_DIV == 1 ? (nfar >= 2 && RT_KNN_DIV_FRAC * nfar >= nact) : nfar >= RT_KNN_DIV;
   }
   // --- bracket the k-th d^2: window [lo, hi), `below` photons under lo
   PROF_CNT(R_KNN_NCALL);

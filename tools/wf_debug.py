@@ -23,4 +23,6 @@ for spp in SPPS:
         rb, ab = g.render(W, W, spp=spp, seed=0x5EED0001, flags=extra | rt.RENDER_WAVEFRONT)
         d = np.abs(ra.astype(np.float64) - rb).max(-1)
         bad = np.argwhere(d > 0)
-        print(f"spp {spp} {name}: {len(bad)} pixels differ, max {d.max():.3g}", [tuple(x) for x in bad[:8]], flush=True)
+        rows = np.unique(bad[:, 0]) if len(bad) else []
+        print(f"spp {spp} {name}: {len(bad)} pixels differ, max {d.max():.3g}", [tuple(int(v) for v in x) for x in bad[:8]],
+              "rows", list(rows[:20]), flush=True)
