@@ -541,6 +541,13 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
 #ifndef RT_NEAREST_FIRST
 #define RT_NEAREST_FIRST 1
 #endif
+// The child being entered is kept as a code (node << 1 | side) and its box reloaded (scalar loads) only
+// when a lane finds a new best hit in the leaf, instead of the 13-SGPR box riding along the whole
+// traversal: at the SGPR limit it was being moved to VGPRs and spilled (C3: 3.22 -> 3.05 ms per frame,
+// scratch writes 2.30 -> 1.58 GB, reads 1.04 -> 0.67 GB; same image; profiles/r04g_*)
+#ifndef RT_NF_CODE
+#define RT_NF_CODE 1
+#endif
 #ifndef RT_NF_TRANS  // nearest-first closest hit in the transparent (non-photon) variants too
 #define RT_NF_TRANS 0
 #endif
@@ -578,7 +585,11 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
   uint64_t act = __ballot(1);
   int sp = 0;
   int32_t N = uni(A.root);
+#if RT_NF_CODE
+  int32_t curCode = 0;    // the child being entered (node << 1 | side): its box is reloaded for the inside test
+#else
   ChildBox cur;           // the box of the child being entered (a leaf's box when N < 0)
+#endif
   while (true) {
     if (N >= 0) {  // internal: both children tested now, the nearer one entered, the other pushed
       const NodeD* nd = S.node + N;
@@ -604,6 +615,19 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
         pkM()[sp] = far;
         if (sp < PK_LDS && in_mask(far)) pkT()[sp * 64 + __lane_id()] = nearLeft ? er : el;
         sp++;
+#if RT_NF_CODE
+        curCode = (N << 1) | (nearLeft ? 0 : 1);
+        act = nearLeft ? L : R;
+        N = nearLeft ? cl.ref : cr.ref;
+      } else if (L) {
+        curCode = N << 1; act = L; N = cl.ref;
+      } else if (R) {
+        curCode = (N << 1) | 1; act = R; N = cr.ref;
+      } else {
+        N = INT32_MAX;
+      }
+      if (N != INT32_MAX) continue;
+#else
         cur = nearLeft ? cl : cr;
         act = nearLeft ? L : R;
       } else if (L) {
@@ -614,6 +638,7 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
         N = INT32_MAX;
       }
       if (N != INT32_MAX) { N = cur.ref; continue; }
+#endif
     } else {  // a leaf: a run of triangles in leaf order
       const int32_t c = ~N;
       const int32_t st = (c >> 5) & LEAF_RUN_MAXSTART, cnt = c & 31;
@@ -631,6 +656,9 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
             bref = st + i;
             // the ray enters the leaf box (the reference's slab arithmetic) clearly before t
             double te;
+#if RT_NF_CODE
+            const ChildBox cur = sload_child(S.node + (curCode >> 1), curCode & 1);
+#endif
             inside = slab_exact(cur.mn, cur.mx, ao, ad, ri, te) && te < t - t * 0x1p-40;
           }
         }
@@ -651,7 +679,11 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
         keep = e <= lim;
       }
       M = __ballot(keep);
+#if RT_NF_CODE
+      if (M) { curCode = code; act = M; N = cb.ref; break; }
+#else
       if (M) { cur = cb; act = M; N = cb.ref; break; }
+#endif
     }
     if (N == INT32_MAX) break;
   }

@@ -86,6 +86,7 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "ld16c99": ["RT_LANE_DIV=16", "RT_LANE_DIV_COS=0.99"],
     "kd1": ["RT_KNN_DIV=1"],                   # ... when half of the call's lanes are far apart
     "ld1": ["RT_LANE_DIV=1"],
+    "nfcode": ["RT_NF_CODE=1"],
     "kd1f4": ["RT_KNN_DIV=1", "RT_KNN_DIV_FRAC=4"],
     "kd1f1": ["RT_KNN_DIV=1", "RT_KNN_DIV_FRAC=1"],
     "kd1r4": ["RT_KNN_DIV=1", "RT_KNN_DIV_R=4.0"],
