@@ -105,5 +105,9 @@ struct rt_scene {
   // counters, two ray queues, the records of levels 1..7
   enum { WF_NODE0, WF_SCOL, WF_TRACED, WF_CNT, WF_Q0, WF_Q1, WF_NODE1, WF_N = WF_NODE1 + 7 };
   void* wf[WF_N] = {};
+  // rt_render_pixels_device: per-sample colours and traced flags of the listed pixels (grow-only)
+  void* smpCol = nullptr;
+  void* smpTr = nullptr;
+  size_t smpCap = 0;  // samples
   size_t wfCap[WF_N] = {};
 };

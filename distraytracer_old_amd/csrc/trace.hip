@@ -379,7 +379,7 @@ int rt_scene_photons(const rt_scene* s, double* pos, double* pwr, int64_t n, int
 
 void rt_scene_destroy(rt_scene* s) {
   if (!s) return;
-  if (!s->allocs.empty() || s->stream || s->outRgb || s->outArgb || !s->tileLists.empty() || s->stage || s->wf[rt_scene::WF_CNT]) {
+  if (!s->allocs.empty() || s->stream || s->outRgb || s->outArgb || !s->tileLists.empty() || s->stage || s->wf[rt_scene::WF_CNT] || s->smpCol) {
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize((hipStream_t)s->stream);
     for (void* p : s->allocs) (void)hipFree(p);
@@ -389,6 +389,8 @@ void rt_scene_destroy(rt_scene* s) {
     (void)hipFree(s->outArgb);
     for (auto& t : s->tileLists) (void)hipFree(t.dev);
     for (void* p : s->wf) (void)hipFree(p);
+    (void)hipFree(s->smpCol);
+    (void)hipFree(s->smpTr);
     if (s->stage) (void)hipHostFree(s->stage);
     if (s->stream) (void)hipStreamDestroy((hipStream_t)s->stream);
   }
@@ -427,6 +429,10 @@ static int make_params(rt_scene* s, const rt_render_params* p, ParamsD& P) {
 #define RT_MAX_G 64
 #endif
   while (G * 2 <= P.spp && G * 2 <= RT_MAX_G) G *= 2;
+  // RT_RENDER_PIXEL_WAVES: one pixel per wave (64 sample lanes, those past spp idle) -- the same
+  // samples in the same order per pixel, so the same image; the multi-GPU split renders its
+  // heaviest tiles this way (their 2 x 2 pixels in four waves at once)
+  if (p->flags & RT_RENDER_PIXEL_WAVES) G = 64;
   static const int TW[7] = {8, 8, 4, 4, 2, 2, 1};  // pixels per wave 64, 32, ..., 1 as tw x th
   int lg = 0;
   while ((1 << lg) < G) ++lg;
@@ -959,6 +965,80 @@ int rt_render_tiles_count(rt_scene* s, const rt_render_params* p, const int32_t*
   if (rc == RT_OK && e != hipSuccess) rc = set_error(RT_E_HIP, hipGetErrorString(e));
   if (rc == RT_OK && se != hipSuccess) rc = set_error(RT_E_HIP, std::string("count kernel: ") + hipGetErrorString(se));
   return rc;
+}
+
+}  // extern "C"
+
+template <uint32_t F>
+static int launch_pixels(rt_scene* s, const SceneD& sd, const ParamsD& P, const int32_t* dpix, int npix, float* d_rgb,
+                         int32_t* d_argb, hipStream_t st) {
+  const int dof = ((F & dv::FT_DOF) && sd.dof && !((F & dv::FT_CAMX) && P.cam != 0)) ? 1 : 0;
+  hipLaunchKernelGGL(dv::sample_kernel<F>, dim3((unsigned)((int64_t)npix * P.spp)), dim3(64), dv::LDS_RENDER_BYTES, st, sd,
+                     P, dpix, (double*)s->smpCol, (uint8_t*)s->smpTr);
+  hipLaunchKernelGGL(dv::pixel_sum_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, P, dpix, npix,
+                     (const double*)s->smpCol, (const uint8_t*)s->smpTr, d_rgb, d_argb, dof);
+  HIPCHK(hipGetLastError());
+  return RT_OK;
+}
+
+extern "C" {
+
+int rt_render_pixels_device(rt_scene* s, const rt_render_params* p, const int32_t* pixels, int npix, float* d_rgb,
+                            int32_t* d_argb, void* stream) {
+  ParamsD P;
+  int rc = make_params(s, p, P);
+  if (rc) return rc;
+  if (P.row0 != 0 || P.nrows != P.H || P.rowStep != 1 || P.band != 1)
+    return set_error(RT_E_INVALID, "rt_render_pixels_device: whole-frame layouts only");
+  if (!pixels || npix <= 0) return set_error(RT_E_INVALID, "rt_render_pixels_device: empty pixel list");
+  if ((int64_t)npix * P.spp > INT32_MAX) return set_error(RT_E_INVALID, "rt_render_pixels_device: too many samples");
+  for (int i = 0; i < npix; ++i)
+    if (pixels[i] < 0 || (int64_t)pixels[i] >= (int64_t)P.W * P.H) return set_error(RT_E_INVALID, "rt_render_pixels_device: pixel out of range");
+  HIPCHK(hipSetDevice(s->device));
+  // the list's device copy: the validated-list cache of the tile lists (a list of ints either way;
+  // its range check there is against the tile count, so bound it by the pixel count here)
+  const int32_t* dpix = nullptr;
+  {
+    rt_scene::TileList* L = nullptr;
+    for (auto& x : s->tileLists)
+      if (x.host.size() == (size_t)npix && std::memcmp(x.host.data(), pixels, sizeof(int32_t) * npix) == 0) { L = &x; break; }
+    if (!L) {
+      if (s->tileLists.size() >= 16) {
+        HIPCHK(hipDeviceSynchronize());
+        (void)hipFree(s->tileLists.front().dev);
+        s->tileLists.erase(s->tileLists.begin());
+      }
+      rt_scene::TileList t;
+      t.host.assign(pixels, pixels + npix);
+      HIPCHK(hipMalloc(&t.dev, sizeof(int32_t) * npix));
+      HIPCHK(hipMemcpy(t.dev, pixels, sizeof(int32_t) * npix, hipMemcpyHostToDevice));
+      s->tileLists.push_back(std::move(t));
+      L = &s->tileLists.back();
+    }
+    dpix = L->dev;
+  }
+  const size_t ns = (size_t)npix * P.spp;
+  if (ns > s->smpCap) {  // grow-only; earlier launches may still read the old buffers: drain the device
+    HIPCHK(hipDeviceSynchronize());
+    (void)hipFree(s->smpCol);
+    (void)hipFree(s->smpTr);
+    s->smpCol = s->smpTr = nullptr;
+    s->smpCap = 0;
+    HIPCHK(hipMalloc(&s->smpCol, ns * 3 * sizeof(double)));
+    HIPCHK(hipMalloc(&s->smpTr, ns));
+    s->smpCap = ns;
+  }
+  SceneD sd = s->dev;
+  sd.fastSlab |= SCENE_NEAREST_FIRST;
+  if (sd.ntop <= 64 && !(p->flags & RT_RENDER_NOWAVECULL)) sd.fastSlab |= SCENE_WAVE_CULL;
+  if (p->flags & RT_RENDER_NOCULL) { sd.topBound = s->noCullBound; sd.fastSlab &= ~(SCENE_NEAREST_FIRST | SCENE_WAVE_CULL); }
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t f = (p->flags & RT_RENDER_GENERIC) ? (uint32_t)dv::FT_ALL : scene_features(s->hs);
+  constexpr uint32_t C4 = dv::FT_PRIM | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX;
+  if (f == 0) return launch_pixels<0u>(s, sd, P, dpix, npix, d_rgb, d_argb, st);
+  if ((f & ~dv::F_C5) == 0) return launch_pixels<dv::F_C5>(s, sd, P, dpix, npix, d_rgb, d_argb, st);
+  if ((f & ~C4) == 0) return launch_pixels<C4>(s, sd, P, dpix, npix, d_rgb, d_argb, st);
+  return launch_pixels<dv::FT_ALL>(s, sd, P, dpix, npix, d_rgb, d_argb, st);
 }
 
 int rt_render_tiles_device(rt_scene* s, const rt_render_params* p, const int32_t* tiles, int ntiles, float* d_rgb,

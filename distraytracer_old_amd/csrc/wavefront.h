@@ -350,3 +350,82 @@ __global__ void __launch_bounds__(64) wf_final_kernel(ParamsD P, int tile0, int 
 
 }  // namespace dv
 }  // namespace rt
+
+namespace rt {
+namespace dv {
+// ---------------------------------------------------------------------------
+// Sample waves (rt_render_pixels_device): the samples of a few listed pixels, ONE sample per wave
+// (lane 0 of a 64-lane workgroup), each colour kept, then every pixel summed in sample order. A
+// pixel's 16 or 64 samples run in parallel on as many SIMDs instead of sharing one wave, whose
+// packet traversal walks the union of their paths: the multi-GPU split renders its heaviest tiles
+// this way so that no single wave outlasts a rank's share of the frame. Same samples, same keys,
+// same order of the per-pixel sum: the same pixels as render_kernel.
+template <uint32_t F>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_RENDER_WAVES)))
+sample_kernel(SceneD S, ParamsD P, const int32_t* __restrict__ pix, double* __restrict__ col, uint8_t* __restrict__ tr) {
+  if (threadIdx.x != 0) return;
+  const int b = blockIdx.x, i = b / P.spp, s = b % P.spp;
+  const int px = pix[i];
+  PixGeo g;
+  g.row = px / P.W;
+  g.col = px % P.W;
+  g.valid = true;
+  g.j = 0; g.pl = 0; g.ci = g.col; g.ri = g.row;
+  const bool dof = (F & FT_DOF) && S.dof && !((F & FT_CAMX) && P.cam != 0);
+  Key k;
+  k.seed = P.seed;
+  k.tsite = SITE_TIME;
+  k.pixel = (uint64_t)g.row * (uint64_t)P.W + (uint64_t)g.col;
+  k.sample = (uint32_t)s;
+  V fpt = mk(0, 0, 0), lc = mk(0, 0, 0);
+  if (dof) {  // shootMultiDpthOfFldRays (myScene.java:1386-1406), as render_kernel
+    const double rayY = (-1 * (g.row - P.H / 2.0)), rayX = g.col - P.W / 2.0;
+    lc = nrmz(mk(rayX, rayY, P.viewZ));
+    const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    V ld = nrmz(nrmz(lc));
+    V fo = xpt(I, mk(0, 0, 0)), fd = xvec(I, ld);
+    V fN = mk(0, 0, 1);
+    double pr = dot(fN, fd);
+    double t = -(dot(fN, fo) + S.lensFocal) / pr;
+    fpt = mk(fd.x * t + fo.x, fd.y * t + fo.y, fd.z * t + fo.z);
+  }
+  V o, d, c = mk(0, 0, 0);
+  const bool traced = wf_camera<F>(S, P, g, s, dof, fpt, lc, k.pixel, o, d);
+  if (traced) {
+    Counters ct;
+    c = trace_sample<false, F>(S, o, d, k, ct);
+  }
+  wf_put(col + 3 * (size_t)b, c);
+  tr[b] = traced ? 1 : 0;
+}
+// the listed pixels' sums in sample order and render_kernel's epilogue (whole-frame layout)
+__global__ void __launch_bounds__(256) pixel_sum_kernel(ParamsD P, const int32_t* __restrict__ pix, int npix,
+                                                        const double* __restrict__ col, const uint8_t* __restrict__ tr,
+                                                        float* __restrict__ rgb, int32_t* __restrict__ argb, int dof) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= npix) return;
+  const int n = P.spp;
+  double rs = 0, gs = 0, bs = 0;
+  for (int s = 0; s < n; ++s) {
+    const size_t b = (size_t)i * n + s;
+    if (n == 1 && !dof) {
+      rs = col[3 * b]; gs = col[3 * b + 1]; bs = col[3 * b + 2];
+    } else if (tr[b]) {
+      rs += col[3 * b]; gs += col[3 * b + 1]; bs += col[3 * b + 2];
+    }
+  }
+  const V c = (n == 1 && !dof) ? mk(rs, gs, bs) : clampc(mk(rs / n, gs / n, bs / n));
+  const size_t o = (size_t)pix[i];
+  if (rgb) {
+    rgb[3 * o + 0] = (float)c.x;
+    rgb[3 * o + 1] = (float)c.y;
+    rgb[3 * o + 2] = (float)c.z;
+  }
+  if (argb) {  // myColor.getInt (myObjShader.java:671)
+    uint32_t v = (uint32_t)(255u << 24) + ((uint32_t)jd2i(c.x * 255) << 16) + ((uint32_t)jd2i(c.y * 255) << 8) +
+                 (uint32_t)jd2i(c.z * 255);
+    argb[o] = (int32_t)v;
+  }
+}
+}  // namespace dv
+}  // namespace rt

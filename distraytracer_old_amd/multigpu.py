@@ -48,6 +48,30 @@ def cost_bucket(costs):
     return np.where(c > 0, np.floor(4.0 * np.log2(np.maximum(c, 1.0))), -1.0)
 
 
+def contiguous_tiles(costs, world: int) -> list:
+    """Cut the tiles in row-major order into `world` contiguous runs of (nearly) equal measured
+    cost (prefix sums; rank r takes the tiles whose cumulative cost midpoint lies in
+    [r T / N, (r + 1) T / N)): every rank renders a compact region of the image, so the waves
+    running together share BVH and texture cache lines. Each rank's list is in dispatch order
+    (longest first by quarter-octave bucket, row-major inside a bucket). Deterministic."""
+    import numpy as np
+
+    c = np.asarray(costs, dtype=np.float64)
+    cum = np.cumsum(c)
+    total = cum[-1] if len(cum) else 0.0
+    mid = cum - 0.5 * c
+    owner = np.minimum((mid * world / max(total, 1e-300)).astype(np.int64), world - 1) if total > 0 else \
+        (np.arange(len(c)) * world // max(1, len(c)))
+    bucket = cost_bucket(c)
+    idx = np.arange(len(c), dtype=np.int64)
+    out = []
+    for r in range(world):
+        t = idx[owner == r]
+        t = t[np.lexsort((t, -bucket[t]))]
+        out.append(t.astype(np.int32))
+    return out
+
+
 def balanced_tiles(costs, world: int) -> list:
     """Deal the tiles of a layout to `world` ranks by their measured costs: tiles sorted by cost
     (descending, ties by index) are dealt serpentine (0..N-1, N-1..0, ...), so the ranks' cost sums
@@ -85,6 +109,60 @@ def tile_pixels(tiles, tiles_x: int, tw: int, th: int, W: int, nrows: int):
     cols = tx[:, None] * tw + dx[None, :]
     ok = (rows < nrows) & (cols < W)
     return (rows * W + cols)[ok]
+
+
+WAVE_SLOTS = 4096  # waves in flight on one MI355X at the render kernel's occupancy: 256 CUs x 4 SIMDs x 4
+
+
+class RankPlan:
+    """One rank's share of a whole-frame layout: wave tiles (rt_render_tiles_device, in dispatch
+    order) and the pixels of its heaviest tiles, rendered one sample per wave beside them
+    (rt_render_pixels_device on a second stream)."""
+
+    def __init__(self, tiles, pixels):
+        import numpy as np
+
+        self.tiles = np.ascontiguousarray(tiles, dtype=np.int32)
+        self.pixels = np.ascontiguousarray(pixels, dtype=np.int32)
+
+    def pixel_list(self, tiles_x: int, tw: int, th: int, W: int, H: int):
+        """Every pixel the plan writes: its tiles' pixels (tile order), then the split pixels."""
+        import numpy as np
+
+        return np.concatenate([tile_pixels(self.tiles, tiles_x, tw, th, W, H), self.pixels.astype(np.int64)])
+
+
+def rank_plans(costs, world: int, tiles_x: int, tw: int, th: int, W: int, H: int, mode: str = "cut",
+               heavy: float = 0.75, slots: int = WAVE_SLOTS) -> list:
+    """Partition a layout's tiles over `world` ranks by their measured wave times (`contiguous_tiles`
+    for mode "cut", `balanced_tiles` for "deal"), then take out of every rank's list the tiles whose
+    own wave would last more than `heavy` x a rank's ideal share (total wave time / (slots x world)):
+    a launch cannot end before its longest wave, so their pixels are rendered one sample per wave
+    (RankPlan.pixels) instead. world == 1: one plan of every tile, nothing split."""
+    import numpy as np
+
+    c = np.asarray(costs, dtype=np.float64)
+    parts = (contiguous_tiles if mode == "cut" else balanced_tiles)(c, world)
+    if world == 1:
+        return [RankPlan(parts[0], [])]
+    thr = heavy * c.sum() / (slots * world)
+    out = []
+    for t in parts:
+        hv = c[t] > thr
+        out.append(RankPlan(t[~hv], tile_pixels(t[hv], tiles_x, tw, th, W, H)))
+    return out
+
+
+def render_plan(scene, p, plan: RankPlan, rgb_ptr: int, argb_ptr: int, stream, side_stream):
+    """Launch a RankPlan: the split pixels on side_stream (after stream's prior work), the tiles on
+    stream, and stream then waits for side_stream: both run at once, the long sample waves first."""
+    if len(plan.pixels):
+        side_stream.wait_stream(stream)
+        scene.render_pixels_device(p, plan.pixels, rgb_ptr, argb_ptr, side_stream.cuda_stream)
+    if len(plan.tiles):
+        scene.render_tiles_device(p, plan.tiles, rgb_ptr, argb_ptr, stream.cuda_stream)
+    if len(plan.pixels):
+        stream.wait_stream(side_stream)
 
 
 def tile_assembler(pix, cap: int, device):
@@ -280,9 +358,11 @@ class RankRenderer:
     from the double colour, so rank 0 receives the 1-GPU ints exactly (packing the gathered float RGB
     again could differ by one in a channel whose double value rounds up to the next float).
 
-    partition "tiles" (default): the frame's wave tiles dealt by measured cost (`balanced_tiles`;
-    rank 0 calibrates, rt_tile_costs, and broadcasts the costs); rank r renders its tile list into a
-    whole-frame buffer (rt_render_tiles_device) and packs its pixels (`tile_pixels`) for the gather.
+    partition "tiles" (default): the frame's wave tiles cut into contiguous runs of equal measured
+    cost (`rank_plans`: rank 0 calibrates, rt_tile_costs, and broadcasts the costs), the tiles whose
+    own wave would outlast a rank's share rendered one sample per wave beside them; rank r renders
+    its plan into a whole-frame buffer (rt_render_tiles_device + rt_render_pixels_device) and packs
+    its pixels for the gather. "deal": the tiles dealt serpentine by cost instead (`balanced_tiles`).
     partition "bands": the interleaved 8-row bands of `rows_of` (rt_render_device).
     `stage_host`: copy the tiles to host memory before the exchange (the gloo backend, which cannot
     gather device tensors; used to run this exact path as several processes on one GPU).
@@ -301,13 +381,13 @@ class RankRenderer:
 
         from . import rt
 
-        assert partition in ("tiles", "bands")
+        assert partition in ("tiles", "deal", "bands")
         assert set(planes) <= {"rgb", "argb"} and planes
         self.scene, self.W, self.H = scene, W, H
         self.dist = dist
         self.rank = dist.get_rank() if dist else 0
         self.world = dist.get_world_size() if dist else 1
-        self.partition = partition if self.world > 1 else "bands"
+        self.partition = ("tiles" if partition == "deal" else partition) if self.world > 1 else "bands"
         self.stream = torch.cuda.current_stream()
         self.stage_host = stage_host
         self.ex = {}
@@ -326,7 +406,7 @@ class RankRenderer:
                 if "argb" in planes:
                     self.ex["argb"] = FrameExchange(dist, H, (self.maxrows, W), xdev, dtype=torch.int32, band=band)
             return
-        # cost-balanced tiles of the whole-frame layout
+        # cost-balanced parts of the whole-frame layout
         self.p = rt.params(W, H, spp=spp, seed=seed)
         self.rows = (0, H, 1, 1)
         ntiles, tiles_x, tw, th = scene.tile_layout(self.p)
@@ -334,9 +414,12 @@ class RankRenderer:
         if self.rank == 0:
             cost.copy_(torch.from_numpy(scene.tile_costs(self.p).astype(np.int64)))
         dist.broadcast(cost, 0)
-        parts = balanced_tiles(cost.cpu().numpy(), self.world)
-        self.tiles = parts[self.rank]
-        pix = [tile_pixels(t, tiles_x, tw, th, W, H) for t in parts]
+        plans = rank_plans(cost.cpu().numpy(), self.world, tiles_x, tw, th, W, H,
+                           mode="cut" if partition == "tiles" else "deal")
+        self.plan = plans[self.rank]
+        self.tiles = self.plan.tiles
+        self.side = torch.cuda.Stream()
+        pix = [pl.pixel_list(tiles_x, tw, th, W, H) for pl in plans]
         self.npix = len(pix[self.rank])
         self.pix = torch.from_numpy(pix[self.rank]).to("cuda")
         cap = max(len(x) for x in pix)
@@ -354,7 +437,7 @@ class RankRenderer:
         rgb = self.rgb if rgb is None else rgb
         argb = self.argb if argb is None else argb
         if self.partition == "tiles":
-            self.scene.render_tiles_device(self.p, self.tiles, rgb.data_ptr(), argb.data_ptr(), self.stream.cuda_stream)
+            render_plan(self.scene, self.p, self.plan, rgb.data_ptr(), argb.data_ptr(), self.stream, self.side)
         else:
             self.scene.render_device(self.p, rgb.data_ptr(), argb.data_ptr(), self.stream.cuda_stream)
         if ev:

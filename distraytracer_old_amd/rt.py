@@ -47,7 +47,8 @@ EXPORTS = ["rt_abi_version", "rt_build_id", "rt_last_error", "rt_device_count", 
            "rt_scene_photon_map", "rt_photons_shoot",
            "rt_photons_set",
            "rt_png_name", "rt_scene_save_name", "rt_math_eval", "rt_tile_layout", "rt_tile_costs",
-           "rt_render_tiles_device", "rt_render_tiles_count", "rt_photon_gather",
+           "rt_render_tiles_device", "rt_render_tiles_count",
+           "rt_render_pixels_device", "rt_photon_gather",
            "rt_photon_kdtree", "rt_scene_photon_kdtree"]
 
 _lib = None
@@ -109,6 +110,8 @@ def lib():
         L.rt_tile_costs.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int]
         L.rt_render_tiles_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.rt_render_pixels_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.rt_render_tiles_count.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int,
                                             ctypes.c_void_p]
         L.rt_photon_kdtree.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
@@ -193,6 +196,7 @@ RENDER_NOCULL = 4  # RT_RENDER_NOCULL: no bounding-sphere culling of top-level p
 RENDER_SHCOMPACT = 8  # RT_RENDER_SHCOMPACT: a wave's shadow rays traced compacted (same image)
 RENDER_NOWAVECULL = 16  # RT_RENDER_NOWAVECULL: no wave-level shadow candidate test (same image)
 RENDER_WAVEFRONT = 32  # RT_RENDER_WAVEFRONT: level-synchronous shading (same image)
+RENDER_PIXEL_WAVES = 64  # RT_RENDER_PIXEL_WAVES: one pixel per wave (same image)
 
 
 def params(W, H, spp=0, seed=0x5EED0001, rows=None, row_step=1, flags=0, row_band=1) -> RenderParams:
@@ -351,6 +355,12 @@ class Scene:
         out = np.zeros_like(pts)
         _check(lib().rt_photon_gather(self._h, pts.ctypes.data, out.ctypes.data, len(pts)), "rt_photon_gather")
         return out
+
+    def render_pixels_device(self, p: RenderParams, pixels: np.ndarray, rgb_ptr: int, argb_ptr: int, stream: int = 0):
+        """Asynchronous one-sample-per-wave render of the listed pixels (host int32 list) into whole-frame buffers."""
+        t = np.ascontiguousarray(pixels, dtype=np.int32)
+        _check(lib().rt_render_pixels_device(self._h, ctypes.byref(p), t.ctypes.data, len(t), ctypes.c_void_p(rgb_ptr),
+                                             ctypes.c_void_p(argb_ptr), ctypes.c_void_p(stream)), "rt_render_pixels_device")
 
     def render_tiles_count(self, p: RenderParams, tiles: np.ndarray) -> dict:
         """Counters (rt_render_count's) of an instrumented render of the listed tiles only."""

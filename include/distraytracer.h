@@ -190,6 +190,9 @@ typedef struct rt_render_params {
    tree is one launch over a compacted ray queue, frames in HBM records, folded bottom up; same image.
    Blocks until the frame is done (it reads each level's ray count); not with tile lists. */
 #define RT_RENDER_WAVEFRONT 32u
+/* one pixel per wave (64 sample lanes; lanes past spp idle) instead of 64 / G pixels of G samples:
+   same samples, same per-pixel order, same image; a layout of width x height one-pixel tiles */
+#define RT_RENDER_PIXEL_WAVES 64u
 
 typedef struct rt_scene rt_scene;
 
@@ -278,6 +281,13 @@ int rt_tile_layout(rt_scene* scene, const rt_render_params* p, int32_t* out);
 int rt_tile_costs(rt_scene* scene, const rt_render_params* p, uint32_t* cost, int cap);
 int rt_render_tiles_device(rt_scene* scene, const rt_render_params* p, const int32_t* tiles, int ntiles, float* d_rgb,
                            int32_t* d_argb, void* hip_stream);
+/* Render only the listed pixels (indices row * width + col of a whole-frame layout: p's rows must be
+   the whole image) with ONE sample per wave -- each pixel's samples run in parallel on as many
+   SIMDs -- and each pixel summed in sample order: the same pixels as the other renders, written into
+   whole-frame DEVICE buffers (other pixels untouched); asynchronous on hip_stream. For the handful of
+   pixels whose shared wave would outlast a GPU's share of a multi-GPU frame (multigpu.py). */
+int rt_render_pixels_device(rt_scene* scene, const rt_render_params* p, const int32_t* pixels, int npix, float* d_rgb,
+                            int32_t* d_argb, void* hip_stream);
 /* Instrumented render of the listed tiles (rt_render_count's counters for those tiles only; blocking). */
 int rt_render_tiles_count(rt_scene* scene, const rt_render_params* p, const int32_t* tiles, int ntiles, uint64_t* stats);
 /* `refine on` (myScene.setRefine, myScene.java:796-803): the progressive steps of a width x height

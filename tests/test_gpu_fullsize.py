@@ -38,6 +38,30 @@ def _split_equals_full(g, W, H, spp, seed, rgb, argb, world=8):
     assert np.array_equal(multigpu.assemble(tr, H).view(np.uint32), rgb.view(np.uint32))
 
 
+def _plan_split_equals_full(g, W, H, spp, seed, rgb, argb, world=8):
+    """bench.py --gpus 8's default split (multigpu.rank_plans: contiguous cost-balanced runs, the
+    heaviest tiles' pixels one sample per wave on a second stream) == the 1-GPU frame."""
+    import torch
+
+    p = rt.params(W, H, spp=spp, seed=seed)
+    n, tx, tw, th = g.tile_layout(p)
+    plans = multigpu.rank_plans(g.tile_costs(p), world, tx, tw, th, W, H)
+    assert sum(len(pl.pixels) for pl in plans) > 0  # the split path is exercised
+    out_rgb = torch.full((H * W, 3), -1.0, device="cuda")
+    out_argb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    b_rgb, b_argb = torch.empty_like(out_rgb), torch.empty_like(out_argb)
+    st, side = torch.cuda.current_stream(), torch.cuda.Stream()
+    for pl in plans:
+        b_rgb.fill_(-2.0)
+        multigpu.render_plan(g, p, pl, b_rgb.data_ptr(), b_argb.data_ptr(), st, side)
+        pix = torch.from_numpy(pl.pixel_list(tx, tw, th, W, H)).cuda()
+        out_rgb[pix] = b_rgb[pix]
+        out_argb[pix] = b_argb[pix]
+    torch.cuda.synchronize()
+    assert np.array_equal(out_argb.cpu().numpy().reshape(H, W), argb)
+    assert np.array_equal(out_rgb.cpu().numpy().reshape(H, W, 3).view(np.uint32), rgb.view(np.uint32))
+
+
 def _tiles_split_equals_full(g, W, H, spp, seed, rgb, argb, world=8):
     """The cost-balanced tile partition of bench.py --gpus 8 (measured costs, balanced_tiles,
     rt_render_tiles_device per rank, pixels scattered back by tile_pixels) == the 1-GPU frame."""
@@ -73,6 +97,7 @@ def test_c4_full_size_properties():
     assert rgb.min() >= 0 and rgb.max() <= 1.0
     _split_equals_full(g, W, H, spp, seed, rgb, argb)
     _tiles_split_equals_full(g, W, H, spp, seed, rgb, argb)
+    _plan_split_equals_full(g, W, H, spp, seed, rgb, argb)
     # oracle rows through the glass bunnies, the columns and the sky (the oracle runs ~3 s a row)
     o = OracleScene(scenes.SCENE_DIR, cli, tex)
     for row in (700, 1300, 1900):
@@ -91,8 +116,18 @@ def test_c5_full_size_properties():
     assert rgb.min() >= 0 and rgb.max() <= 1.0
     _split_equals_full(g, W, H, spp, seed, rgb, argb)
     _tiles_split_equals_full(g, W, H, spp, seed, rgb, argb)
+    _plan_split_equals_full(g, W, H, spp, seed, rgb, argb)
     o = OracleScene(scenes.SCENE_DIR, cli)
     o.set_photons(*g.photons())
     for row in (100, 400, 640, 900):  # ceiling light, spheres (mirror / glass: caustics), floor
         ro, ao, _ = o.render(W, H, spp=spp, seed=seed, rows=(row, row + 1))
         assert_exact_decisions(compare(rgb[row:row + 1], argb[row:row + 1], ro, ao))
+
+
+def test_c3_full_size_plan_split():
+    """The headline config's 8-rank split (contiguous cost-balanced runs + the heaviest tiles' pixels
+    one sample per wave) reassembles to the 1-GPU frame bit for bit."""
+    cli, W, H, spp, seed = scenes.CONFIGS["C3"]
+    g = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+    rgb, argb = g.render(W, H, spp=spp, seed=seed)
+    _plan_split_equals_full(g, W, H, spp, seed, rgb, argb)

@@ -389,6 +389,33 @@ def test_wavefront_c4_oracle_parity():
     assert_exact_decisions(compare(rg, ag, ro, ao))
 
 
+@pytest.mark.parametrize("cli,W,spp", [("c3_bun69k.cli", 128, 4), ("plnts3ColsBunnies.cli", 96, 4), ("t11.cli", 64, 2),
+                                       ("p2_t07.cli", 96, 2), ("old_t10.cli", 96, 4), ("t01.cli", 96, 1),
+                                       ("p3_t11_sierp.cli", 64, 1)])
+def test_sample_waves_render_identically(cli, W, spp):
+    """rt_render_pixels_device (one sample per wave, each pixel summed in sample order afterwards: the
+    multi-GPU split's heaviest tiles) writes exactly the listed pixels of the plain render, and no
+    other: glass, photon map, DOF, fisheye (untraced samples outside the image circle), 1 spp, instances."""
+    import torch
+
+    scenes.ensure_bun69k()
+    g = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+    ra, aa = g.render(W, W, spp=spp, seed=SEED)
+    rng = np.random.default_rng(W + spp)
+    pix = np.unique(rng.integers(0, W * W, size=W * W // 5)).astype(np.int32)
+    rgb = torch.full((W * W, 3), -1.0, device="cuda")
+    argb = torch.zeros(W * W, dtype=torch.int32, device="cuda")
+    g.render_pixels_device(rt.params(W, W, spp=spp, seed=SEED), pix, rgb.data_ptr(), argb.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rb, ab = rgb.cpu().numpy(), argb.cpu().numpy()
+    mask = np.zeros(W * W, bool)
+    mask[pix] = True
+    assert np.array_equal(ab[mask], aa.reshape(-1)[mask])
+    assert np.array_equal(rb[mask].view(np.uint32), ra.reshape(-1, 3)[mask].view(np.uint32))
+    assert (rb[~mask] == -1.0).all()
+
+
 def test_photon_shards_merge_to_the_full_prepass(tmp_path):
     """Multi-GPU photon pre-pass (8(e)): shards shot separately and merged in rank order give
     the single-GPU photon_list bit for bit, and the same image."""

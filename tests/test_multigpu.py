@@ -295,3 +295,25 @@ def test_gloo_world3_tile_partition_reassembles():
         assert p.exitcode == 0
     expect = np.stack([np.arange(H * W) + 1000 * f for f in range(3)]).astype(np.float32)
     assert np.array_equal(frames, expect)
+
+
+def test_rank_plans_cover_the_frame_and_split_only_heavy_tiles():
+    """multigpu.rank_plans (bench.py --gpus N's default split): contiguous runs of equal cost, every
+    pixel exactly once, and only tiles costlier than heavy x a rank's ideal share (total / (4096 x N))
+    become one-sample-per-wave pixels."""
+    rng = np.random.default_rng(3)
+    W, H, tw, th = 256, 200, 2, 2
+    tx = W // tw
+    n = tx * (H // th)
+    costs = (rng.pareto(2.0, n) * 20 + 5).astype(np.int64)
+    costs[rng.choice(n, 5, replace=False)] = 10 ** 7  # five outliers
+    for world in (2, 3, 8):
+        plans = multigpu.rank_plans(costs, world, tx, tw, th, W, H)
+        pix = np.concatenate([pl.pixel_list(tx, tw, th, W, H) for pl in plans])
+        assert np.array_equal(np.sort(pix), np.arange(W * H))
+        thr = 0.75 * costs.sum() / (multigpu.WAVE_SLOTS * world)
+        assert sum(len(pl.pixels) for pl in plans) == 4 * int((costs > thr).sum())
+        for pl in plans:
+            assert (costs[pl.tiles] <= thr).all()
+    one = multigpu.rank_plans(costs, 1, tx, tw, th, W, H)
+    assert len(one) == 1 and len(one[0].pixels) == 0 and len(one[0].tiles) == n

@@ -25,7 +25,13 @@ if "--flags" in argv:
     i = argv.index("--flags")
     FLAGS = int(argv[i + 1])
     del argv[i:i + 2]
+HEAVY = 1e30
+if "--heavy" in argv:
+    i = argv.index("--heavy")
+    HEAVY = float(argv[i + 1])
+    del argv[i:i + 2]
 TILES = "--tiles" in argv
+CUT = "--cut" in argv
 args = [a for a in argv if not a.startswith("--")]
 BANDS = [int(x) for x in args[0].split(",")] if args else [multigpu.BAND]
 CFG = args[1] if len(args) > 1 else "C3"
@@ -36,18 +42,19 @@ s = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
 s.build_photons(seed)
 
 
-def time_tiles(p, tiles, iters=5, warm=2):
+def time_plan(p, plan, iters=5, warm=2):
     import torch
 
     rgb = torch.empty((H * W, 3), dtype=torch.float32, device="cuda")
     argb = torch.empty((H * W,), dtype=torch.int32, device="cuda")
     st = torch.cuda.current_stream()
+    side = torch.cuda.Stream()
     for _ in range(warm):
-        s.render_tiles_device(p, tiles, rgb.data_ptr(), argb.data_ptr(), st.cuda_stream)
+        multigpu.render_plan(s, p, plan, rgb.data_ptr(), argb.data_ptr(), st, side)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(iters):
-        s.render_tiles_device(p, tiles, rgb.data_ptr(), argb.data_ptr(), st.cuda_stream)
+        multigpu.render_plan(s, p, plan, rgb.data_ptr(), argb.data_ptr(), st, side)
     e1.record(st)
     e1.synchronize()
     return e0.elapsed_time(e1) / iters
@@ -60,8 +67,11 @@ for flags, name in ORDERS:
         p = rt.params(W, H, spp=spp, seed=seed, flags=flags)
         costs = s.tile_costs(p)
         for world in WORLDS:
-            ts = [time_tiles(p, t) for t in multigpu.balanced_tiles(costs, world)]
-            print(" ", "tiles N", world, "max %.3f mean %.3f ideal %.3f eff %.3f" % (
+            n, tx, tw, th = s.tile_layout(p)
+            plans = multigpu.rank_plans(costs, world, tx, tw, th, W, H, mode="cut" if CUT else "deal",
+                                        heavy=HEAVY)
+            ts = [time_plan(p, pl) for pl in plans]
+            print(" ", "cut" if CUT else "tiles", "heavy", HEAVY, "split px", sum(len(pl.pixels) for pl in plans), "N", world, "max %.3f mean %.3f ideal %.3f eff %.3f" % (
                 max(ts), sum(ts) / len(ts), full / world, full / world / max(ts)),
                 "per rank", " ".join("%.3f" % t for t in ts), flush=True)
         continue

@@ -15,11 +15,12 @@ from distraytracer_old_amd import rt, scenes  # noqa: E402
 
 CFG = sys.argv[1] if len(sys.argv) > 1 else "C5"
 TOP = int(sys.argv[2]) if len(sys.argv) > 2 else 12
+FLAGS = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 cli, W, H, spp, seed = scenes.CONFIGS[CFG]
 scenes.ensure_bun69k()
 s = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
 s.build_photons(seed)
-p = rt.params(W, H, spp=spp, seed=seed)
+p = rt.params(W, H, spp=spp, seed=seed, flags=FLAGS)
 n, tx, tw, th = s.tile_layout(p)
 c = s.tile_costs(p).astype(np.float64) * 0.01  # us
 print(f"{CFG}: {n} tiles of {tw}x{th} px; wave time us: mean {c.mean():.1f} p50 {np.median(c):.1f} "
