@@ -116,14 +116,17 @@ WAVE_SLOTS = 4096  # waves in flight on one MI355X at the render kernel's occupa
 
 class RankPlan:
     """One rank's share of a whole-frame layout: wave tiles (rt_render_tiles_device, in dispatch
-    order) and the pixels of its heaviest tiles, rendered one sample per wave beside them
-    (rt_render_pixels_device on a second stream)."""
+    order) and the pixels of its heaviest tiles, rendered beside them on a second stream -- one pixel
+    per wave (RT_RENDER_PIXEL_WAVES, mode "pixel": a 2 x 2-pixel tile's four pixels in four waves) or,
+    when the layout already holds one pixel per wave, one sample per wave (rt_render_pixels_device,
+    mode "sample")."""
 
-    def __init__(self, tiles, pixels):
+    def __init__(self, tiles, pixels, mode="pixel"):
         import numpy as np
 
         self.tiles = np.ascontiguousarray(tiles, dtype=np.int32)
         self.pixels = np.ascontiguousarray(pixels, dtype=np.int32)
+        self.mode = mode
 
     def pixel_list(self, tiles_x: int, tw: int, th: int, W: int, H: int):
         """Every pixel the plan writes: its tiles' pixels (tile order), then the split pixels."""
@@ -146,10 +149,11 @@ def rank_plans(costs, world: int, tiles_x: int, tw: int, th: int, W: int, H: int
     if world == 1:
         return [RankPlan(parts[0], [])]
     thr = heavy * c.sum() / (slots * world)
+    mode = "sample" if tw * th == 1 else "pixel"
     out = []
     for t in parts:
         hv = c[t] > thr
-        out.append(RankPlan(t[~hv], tile_pixels(t[hv], tiles_x, tw, th, W, H)))
+        out.append(RankPlan(t[~hv], tile_pixels(t[hv], tiles_x, tw, th, W, H), mode))
     return out
 
 
@@ -158,7 +162,14 @@ def render_plan(scene, p, plan: RankPlan, rgb_ptr: int, argb_ptr: int, stream, s
     stream, and stream then waits for side_stream: both run at once, the long sample waves first."""
     if len(plan.pixels):
         side_stream.wait_stream(stream)
-        scene.render_pixels_device(p, plan.pixels, rgb_ptr, argb_ptr, side_stream.cuda_stream)
+        if plan.mode == "sample":
+            scene.render_pixels_device(p, plan.pixels, rgb_ptr, argb_ptr, side_stream.cuda_stream)
+        else:  # one-pixel tiles of the RT_RENDER_PIXEL_WAVES layout: tile index == pixel index
+            from . import rt
+
+            pp = rt.RenderParams(*[getattr(p, f) for f, _ in p._fields_])
+            pp.flags = p.flags | rt.RENDER_PIXEL_WAVES
+            scene.render_tiles_device(pp, plan.pixels, rgb_ptr, argb_ptr, side_stream.cuda_stream)
     if len(plan.tiles):
         scene.render_tiles_device(p, plan.tiles, rgb_ptr, argb_ptr, stream.cuda_stream)
     if len(plan.pixels):

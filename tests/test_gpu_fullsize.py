@@ -38,7 +38,7 @@ def _split_equals_full(g, W, H, spp, seed, rgb, argb, world=8):
     assert np.array_equal(multigpu.assemble(tr, H).view(np.uint32), rgb.view(np.uint32))
 
 
-def _plan_split_equals_full(g, W, H, spp, seed, rgb, argb, world=8):
+def _plan_split_equals_full(g, W, H, spp, seed, rgb, argb, world=8, expect_split=True):
     """bench.py --gpus 8's default split (multigpu.rank_plans: contiguous cost-balanced runs, the
     heaviest tiles' pixels one sample per wave on a second stream) == the 1-GPU frame."""
     import torch
@@ -46,7 +46,8 @@ def _plan_split_equals_full(g, W, H, spp, seed, rgb, argb, world=8):
     p = rt.params(W, H, spp=spp, seed=seed)
     n, tx, tw, th = g.tile_layout(p)
     plans = multigpu.rank_plans(g.tile_costs(p), world, tx, tw, th, W, H)
-    assert sum(len(pl.pixels) for pl in plans) > 0  # the split path is exercised
+    if expect_split:  # the one-sample-per-wave path is exercised (C4's tiles are all short: none split)
+        assert sum(len(pl.pixels) for pl in plans) > 0
     out_rgb = torch.full((H * W, 3), -1.0, device="cuda")
     out_argb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     b_rgb, b_argb = torch.empty_like(out_rgb), torch.empty_like(out_argb)
@@ -97,7 +98,7 @@ def test_c4_full_size_properties():
     assert rgb.min() >= 0 and rgb.max() <= 1.0
     _split_equals_full(g, W, H, spp, seed, rgb, argb)
     _tiles_split_equals_full(g, W, H, spp, seed, rgb, argb)
-    _plan_split_equals_full(g, W, H, spp, seed, rgb, argb)
+    _plan_split_equals_full(g, W, H, spp, seed, rgb, argb, expect_split=False)
     # oracle rows through the glass bunnies, the columns and the sky (the oracle runs ~3 s a row)
     o = OracleScene(scenes.SCENE_DIR, cli, tex)
     for row in (700, 1300, 1900):
