@@ -112,16 +112,19 @@ def tile_pixels(tiles, tiles_x: int, tw: int, th: int, W: int, nrows: int):
 
 
 WAVE_SLOTS = 4096  # waves in flight on one MI355X at the render kernel's occupancy: 256 CUs x 4 SIMDs x 4
+# rank_plans' split threshold, in units of a rank's ideal per-slot share. Chosen on the MI355X by
+# tools/band_timing.py (profiles/r04q_plan_*.log, N=8 emulated): C3 0.71 (1.0) / 0.81 (1.25) /
+# 0.68 (1.5) with one sample per wave, 0.74 with one pixel per wave; C5 0.96 (1.0) / 0.85 (0.75).
+HEAVY = 1.25
 
 
 class RankPlan:
     """One rank's share of a whole-frame layout: wave tiles (rt_render_tiles_device, in dispatch
-    order) and the pixels of its heaviest tiles, rendered beside them on a second stream -- one pixel
-    per wave (RT_RENDER_PIXEL_WAVES, mode "pixel": a 2 x 2-pixel tile's four pixels in four waves) or,
-    when the layout already holds one pixel per wave, one sample per wave (rt_render_pixels_device,
-    mode "sample")."""
+    order) and the pixels of its heaviest tiles, rendered beside them on a second stream -- one sample
+    per wave (rt_render_pixels_device, mode "sample") or one pixel per wave (RT_RENDER_PIXEL_WAVES,
+    mode "pixel": a 2 x 2-pixel tile's four pixels in four waves)."""
 
-    def __init__(self, tiles, pixels, mode="pixel"):
+    def __init__(self, tiles, pixels, mode="sample"):
         import numpy as np
 
         self.tiles = np.ascontiguousarray(tiles, dtype=np.int32)
@@ -136,12 +139,13 @@ class RankPlan:
 
 
 def rank_plans(costs, world: int, tiles_x: int, tw: int, th: int, W: int, H: int, mode: str = "cut",
-               heavy: float = 0.75, slots: int = WAVE_SLOTS) -> list:
+               heavy: float = HEAVY, slots: int = WAVE_SLOTS, split: str = "sample") -> list:
     """Partition a layout's tiles over `world` ranks by their measured wave times (`contiguous_tiles`
     for mode "cut", `balanced_tiles` for "deal"), then take out of every rank's list the tiles whose
     own wave would last more than `heavy` x a rank's ideal share (total wave time / (slots x world)):
     a launch cannot end before its longest wave, so their pixels are rendered one sample per wave
-    (RankPlan.pixels) instead. world == 1: one plan of every tile, nothing split."""
+    (RankPlan.pixels) instead: one sample per wave (split "sample", the measured best), one pixel per wave
+    (RT_RENDER_PIXEL_WAVES, "pixel"), or "auto" (pixel when a tile holds several pixels). world == 1: one plan of every tile, nothing split."""
     import numpy as np
 
     c = np.asarray(costs, dtype=np.float64)
@@ -149,7 +153,7 @@ def rank_plans(costs, world: int, tiles_x: int, tw: int, th: int, W: int, H: int
     if world == 1:
         return [RankPlan(parts[0], [])]
     thr = heavy * c.sum() / (slots * world)
-    mode = "sample" if tw * th == 1 else "pixel"
+    mode = split if split != "auto" else ("sample" if tw * th == 1 else "pixel")
     out = []
     for t in parts:
         hv = c[t] > thr

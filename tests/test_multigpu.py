@@ -300,7 +300,7 @@ def test_gloo_world3_tile_partition_reassembles():
 def test_rank_plans_cover_the_frame_and_split_only_heavy_tiles():
     """multigpu.rank_plans (bench.py --gpus N's default split): contiguous runs of equal cost, every
     pixel exactly once, and only tiles costlier than heavy x a rank's ideal share (total / (4096 x N))
-    become one-sample-per-wave pixels."""
+    become one-sample-per-wave pixels; split "auto" on a multi-pixel layout picks per-pixel waves."""
     rng = np.random.default_rng(3)
     W, H, tw, th = 256, 200, 2, 2
     tx = W // tw
@@ -311,9 +311,11 @@ def test_rank_plans_cover_the_frame_and_split_only_heavy_tiles():
         plans = multigpu.rank_plans(costs, world, tx, tw, th, W, H)
         pix = np.concatenate([pl.pixel_list(tx, tw, th, W, H) for pl in plans])
         assert np.array_equal(np.sort(pix), np.arange(W * H))
-        thr = 0.75 * costs.sum() / (multigpu.WAVE_SLOTS * world)
+        thr = multigpu.HEAVY * costs.sum() / (multigpu.WAVE_SLOTS * world)
         assert sum(len(pl.pixels) for pl in plans) == 4 * int((costs > thr).sum())
         for pl in plans:
             assert (costs[pl.tiles] <= thr).all()
+            assert pl.mode == "sample"
+    assert all(pl.mode == "pixel" for pl in multigpu.rank_plans(costs, 8, tx, tw, th, W, H, split="auto"))
     one = multigpu.rank_plans(costs, 1, tx, tw, th, W, H)
     assert len(one) == 1 and len(one[0].pixels) == 0 and len(one[0].tiles) == n

@@ -30,6 +30,11 @@ if "--heavy" in argv:
     i = argv.index("--heavy")
     HEAVY = float(argv[i + 1])
     del argv[i:i + 2]
+SPLIT = "auto"
+if "--split" in argv:
+    i = argv.index("--split")
+    SPLIT = argv[i + 1]
+    del argv[i:i + 2]
 TILES = "--tiles" in argv
 CUT = "--cut" in argv
 args = [a for a in argv if not a.startswith("--")]
@@ -42,7 +47,7 @@ s = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
 s.build_photons(seed)
 
 
-def time_plan(p, plan, iters=5, warm=2):
+def time_plan(p, plan, iters=20, warm=3):
     import torch
 
     rgb = torch.empty((H * W, 3), dtype=torch.float32, device="cuda")
@@ -69,9 +74,9 @@ for flags, name in ORDERS:
         for world in WORLDS:
             n, tx, tw, th = s.tile_layout(p)
             plans = multigpu.rank_plans(costs, world, tx, tw, th, W, H, mode="cut" if CUT else "deal",
-                                        heavy=HEAVY)
+                                        heavy=HEAVY, split=SPLIT)
             ts = [time_plan(p, pl) for pl in plans]
-            print(" ", "cut" if CUT else "tiles", "heavy", HEAVY, "split px", sum(len(pl.pixels) for pl in plans), "N", world, "max %.3f mean %.3f ideal %.3f eff %.3f" % (
+            print(" ", "cut" if CUT else "tiles", "heavy", HEAVY, SPLIT, "split px", sum(len(pl.pixels) for pl in plans), "N", world, "max %.3f mean %.3f ideal %.3f eff %.3f" % (
                 max(ts), sum(ts) / len(ts), full / world, full / world / max(ts)),
                 "per rank", " ".join("%.3f" % t for t in ts), flush=True)
         continue
