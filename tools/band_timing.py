@@ -30,7 +30,7 @@ if "--heavy" in argv:
     i = argv.index("--heavy")
     HEAVY = float(argv[i + 1])
     del argv[i:i + 2]
-SPLIT = "auto"
+SPLIT = "sample"
 if "--split" in argv:
     i = argv.index("--split")
     SPLIT = argv[i + 1]
