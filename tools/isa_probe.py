@@ -26,7 +26,7 @@ def main():
         p = Path(td) / "probe.hip"
         p.write_text(src)
         out = Path(td) / "probe.s"
-        r = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *(["-g"] if lines else []), "-I", str(CSRC), *extra, "-S",
+        r = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *(["-gline-tables-only"] if lines else []), "-I", str(CSRC), *extra, "-S",
                             str(p), "-o", str(out)],
                            capture_output=True, text=True)
         if r.returncode:
@@ -53,7 +53,7 @@ def main():
                 bydepth[min(depth, 6)] += 1
                 if depth >= 2:
                     deep["st" if "store" in op else "ld"] += 1
-                    where[(depth, "st" if "store" in op else "ld", loc)] += 1
+                where[(depth, "st" if "store" in op else "ld", loc)] += 1
     desc = s[s.index(".amdhsa_kernel " + m.group(1)):]
     g = lambda k: int(re.search(r"\.%s\s+(\d+)" % k, desc).group(1))
     priv = c.pop("_priv", 0)
@@ -63,7 +63,7 @@ def main():
           f"private={g('amdhsa_private_segment_fixed_size')} vgpr_next={g('amdhsa_next_free_vgpr')} "
           f"sgpr_next={g('amdhsa_next_free_sgpr')} by_depth={dict(sorted(bydepth.items()))}")
     if lines:  # -g changes scheduling slightly: counts are indicative
-        for (dp, kind, lc), v in sorted(where.items(), key=lambda x: -x[1])[:40]:
+        for (dp, kind, lc), v in sorted(where.items(), key=lambda x: (-x[0][0], -x[1]))[:60]:
             print(f"  depth {dp} {kind} {lc}: {v}")
 
 

@@ -96,6 +96,8 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "kd32": ["RT_KNN_DIV=32"],
     "wf5": ["RT_WF_WAVES=5"],                  # level-synchronous kernels at 5 / 3 waves per SIMD
     "wf3": ["RT_WF_WAVES=3"],
+    "head": [],                                # a copy of the in-tree library (the A of an A/B)
+    "flate": [],                               # shade_node's local colour stored into the frame only when it pushes
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
