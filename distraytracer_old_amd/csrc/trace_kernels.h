@@ -2493,10 +2493,12 @@ template <uint32_t F>
 using FrameOf = typename std::conditional<(F & FT_TRANS) != 0, FrameT<F>, FrameR<F>>::type;
 
 // getColorAtPos (myObjShader.java:409-438; simple shader :635-651): local colour and the
-// children. Returns the number of children (0..2); child A is written to `a`.
+// children. Returns the number of children (0..2); child A is written to `a`, the local colour to
+// `loc` -- not to the frame: the caller stores it there only when the node pushes one (a node
+// without children keeps it in registers; the frame stack lives in scratch).
 template <bool CNT, uint32_t F>
-DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key& k, FrameOf<F>& Fr, Child& a,
-                    bool& branch, Counters& ct) {
+DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key& k, FrameOf<F>& Fr, V& loc,
+                    Child& a, bool& branch, Counters& ct) {
   const MatD& m = S.mat[h.mat];
   double r = m.ambient[0], g = m.ambient[1], b = m.ambient[2];
   if constexpr ((F & FT_PHOTON) != 0) {
@@ -2531,7 +2533,7 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
   }
   PROF_ADD(t_ls, R_LIGHT);
   r += ls.x; g += ls.y; b += ls.z;
-  Fr.local = mk(r, g, b);
+  loc = mk(r, g, b);
   branch = (in.gen < S.numRays - 2) && m.hasCaustic;
 #ifdef RT_PROF_NOSECONDARY  // profiling builds only: results differ
   branch = false;
@@ -2642,15 +2644,17 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
         bool branch;
         Child a;
         FrameOf<F>& Fr = fr[sp];
+        V loc;
         PROF_T0(t_sh);
-        int nch = shade_node<CNT, F>(S, h, in, k, Fr, a, branch, ct);
+        int nch = shade_node<CNT, F>(S, h, in, k, Fr, loc, a, branch, ct);
         PROF_ADD(t_sh, R_SHADE);
         if (nch > 0 && sp < MAX_FRAMES) {
+          Fr.local = loc;
           sp++;
           in = a;  // STASH_SHADE: its o / d are already in the LDS slots (shade_node)
           continue;
         }
-        c = branch ? clampc(add(Fr.local, mk(0, 0, 0))) : clampc(Fr.local);  // no child: acc stayed 0
+        c = branch ? clampc(add(loc, mk(0, 0, 0))) : clampc(loc);  // no child: acc stayed 0
       }
     }
     // deliver finished colours upward

@@ -128,13 +128,14 @@ DEVI WfOut wf_shade(const SceneD& S, const Child& in, Key& k, WfNode& rec) {
   bool branch;
   FrameOf<F> Fr;
   Child a;
-  const int nch = shade_node<false, F>(S, h, in, k, Fr, a, branch, ct);
+  V loc;
+  const int nch = shade_node<false, F>(S, h, in, k, Fr, loc, a, branch, ct);
   if (nch == 0) {
-    r.c = branch ? clampc(add(Fr.local, mk(0, 0, 0))) : clampc(Fr.local);
+    r.c = branch ? clampc(add(loc, mk(0, 0, 0))) : clampc(loc);
     return r;
   }
   rec.kind = 1;
-  rec.local[0] = Fr.local.x; rec.local[1] = Fr.local.y; rec.local[2] = Fr.local.z;
+  rec.local[0] = loc.x; rec.local[1] = loc.y; rec.local[2] = loc.z;
   rec.mat = Fr.mat;
   rec.phase = Fr.phase;
   r.a = a;
