@@ -545,13 +545,26 @@ static int sort_tiles(rt_scene::TileSchedule& e, hipStream_t st) {
   if (r != hipSuccess) return set_error(RT_E_HIP, std::string("tile schedule: ") + hipGetErrorString(r));
   // sort key: cost in quarter-octave buckets; tiles of one bucket keep row-major order, so
   // waves running at the same time stay spatially close (shared cache lines) while the
-  // order stays longest-first to within 19 %
-  std::vector<int32_t> order(e.ntiles), key(e.ntiles);
+  // order stays longest-first to within 19 %. A counting sort over the buckets (stable, O(n)):
+  // C4's 1 M tiles sort in a few ms, where std::stable_sort took ~100 ms of the first frames.
+  constexpr int NB = 4 * 32 + 1;  // bucket 0: cost 0; bucket 1 + floor(4 log2 c) for c >= 1
+  std::vector<uint8_t> key(e.ntiles);
+  int hist[NB] = {0};
   for (int i = 0; i < e.ntiles; ++i) {
-    order[i] = i;
-    key[i] = cost[i] ? (int32_t)std::floor(4.0 * std::log2((double)cost[i])) : -1;
+    const uint32_t c = cost[i];
+    int k = 0;
+    if (c) {
+      const int oct = 31 - __builtin_clz(c);
+      const double f = (double)c / (double)(1u << oct);  // [1, 2)
+      k = 1 + 4 * oct + (f >= 1.6817928305074290) + (f >= 1.4142135623730951) + (f >= 1.1892071150027210);
+    }
+    key[i] = (uint8_t)k;
+    hist[k]++;
   }
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key[a] > key[b]; });
+  int start[NB];
+  for (int k = NB - 1, acc = 0; k >= 0; --k) { start[k] = acc; acc += hist[k]; }  // longest first
+  std::vector<int32_t> order(e.ntiles);
+  for (int i = 0; i < e.ntiles; ++i) order[start[key[i]]++] = i;
   HIPCHK(hipMemcpy(e.order, order.data(), sizeof(int32_t) * e.ntiles, hipMemcpyHostToDevice));
   return RT_OK;
 }

@@ -2590,9 +2590,9 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
       a.d = rd;
       if (STASH_SHADE) stash3(SL_RAYD, a.d);
       a.ktm = -1;
-      Fr.phase = 1;
       Fr.mat = h.mat;
-      if constexpr ((F & FT_TRANS) != 0) {
+      if constexpr ((F & FT_TRANS) != 0) {  // FrameR's fold reads only local and mat
+        Fr.phase = 1;
         Fr.mode = FM_REFL;
         Fr.hasB = 0;
       }
@@ -2606,6 +2606,23 @@ DEVI int shade_node(const SceneD& S, const HitRec& h, const Child& in, const Key
 DEVI V clampc(V c) { return mk(jmin(1, c.x), jmin(1, c.y), jmin(1, c.z)); }  // myColor ctor
 
 static constexpr int MAX_FRAMES = 7;  // gen < numRays-2 = 6 -> at most 6 nodes with children
+
+// A lane whose shading tree is finished waits, with its colour, until the wave's last lane leaves
+// the loop. Held in VGPRs, that colour is live across every later iteration of the other lanes'
+// trees, and at 128 VGPRs the compiler spilled it to scratch and reloaded it on every iteration
+// (C3: ~30 B of scratch writes per sample). It waits in the lane's own LDS stash slots instead:
+// every LDS slot the other lanes write while tracing and shading is their own ([slot][lane]:
+// traversal levels, stash slots), except the per-lane stacks of the photon scans and of the
+// lane-wise BVH experiment (RT_LANE_DIV), which index [level][lane] ints over the same bytes -- so
+// not in photon variants nor with RT_LANE_DIV. Measured (profiles/r04z_res_lds_ab.txt): C3 writes
+// 1.36 -> 1.31 GB per frame at the same time; C4's transparent variant lost 1.8 % (its allocation
+// shifts), so it keeps its VGPRs.
+#ifndef RT_RES_LDS
+#define RT_RES_LDS 1
+#endif
+enum { SL_RES = SL_RGB };
+template <uint32_t F>
+static constexpr bool RES_LDS = RT_RES_LDS != 0 && STASH_SHADE && (F & (FT_PHOTON | FT_TRANS)) == 0 && RT_LANE_DIV == 0;
 
 // reflectRay (myScene.java:907-914) for the whole shading tree of one camera sample
 template <bool CNT, uint32_t F>
@@ -2632,10 +2649,12 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
       if (b.t == DMAX) {
         PROF_T0(t_bg);
         c = background<CNT, F>(S, w, ct);
+        if constexpr (RES_LDS<F>) { stash3(SL_RES, c); lds_barrier(); }
         PROF_ADD(t_bg, R_BG);
 #ifdef RT_PROF_NOSHADE
       } else if (true) {
         c = mk(b.t * 0.01, 0, 0);
+        if constexpr (RES_LDS<F>) { stash3(SL_RES, c); lds_barrier(); }
 #endif
       } else {
         PROF_T0(t_hit);
@@ -2655,7 +2674,12 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
           continue;
         }
         c = branch ? clampc(add(loc, mk(0, 0, 0))) : clampc(loc);  // no child: acc stayed 0
+        if constexpr (RES_LDS<F>) { stash3(SL_RES, c); lds_barrier(); }
       }
+    }
+    if constexpr (RES_LDS<F>) {  // the ray's colour reaches the fold through the lane's LDS slots
+      lds_barrier();
+      c = unstash3(SL_RES);
     }
     // deliver finished colours upward
     bool spawned = false;
@@ -2698,8 +2722,19 @@ DEVI V trace_sample(const SceneD& S, V org, V dir, Key k, Counters& ct) {
         sp--;
       }
     }
-    if (!spawned) return c;
+    if (!spawned) {
+      if constexpr (RES_LDS<F>) {  // the finished colour waits in the lane's LDS slots (below)
+        stash3(SL_RES, c);
+        break;
+      }
+      return c;
+    }
   }
+  if constexpr (RES_LDS<F>) {
+    lds_barrier();
+    return unstash3(SL_RES);
+  }
+  __builtin_unreachable();
 }
 
 // ---------------------------------------------------------------------------

@@ -137,7 +137,7 @@ DEVI WfOut wf_shade(const SceneD& S, const Child& in, Key& k, WfNode& rec) {
   rec.kind = 1;
   rec.local[0] = loc.x; rec.local[1] = loc.y; rec.local[2] = loc.z;
   rec.mat = Fr.mat;
-  rec.phase = Fr.phase;
+  rec.phase = ((F & FT_TRANS) != 0) ? Fr.phase : 1;
   r.a = a;
   if constexpr ((F & FT_TRANS) != 0) {
     rec.mode = Fr.mode;

@@ -98,6 +98,8 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "wf3": ["RT_WF_WAVES=3"],
     "head": [],                                # a copy of the in-tree library (the A of an A/B)
     "flate": [],                               # shade_node's local colour stored into the frame only when it pushes
+    "reslds": [],                              # a finished sample's colour waits in LDS, not in spilled VGPRs
+    "reslds0": ["RT_RES_LDS=0"],
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
