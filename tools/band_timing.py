@@ -2,12 +2,14 @@
 """Per-rank kernel time of the multi-GPU partitions, emulated on one GPU: max over ranks vs
 full-frame/N (strong-scaling efficiency of the kernel alone).
 
-  tools/band_timing.py [BANDS] [CFG] [--tiles] [--worlds 2,4,8]
+  tools/band_timing.py [BANDS] [CFG] [--tiles [--cut] [--heavy H] [--split sample|pixel|auto]]
+                       [--worlds 2,4,8] [--flags F]
 
 bands: rank r renders the interleaved row bands of multigpu.rows_of (rt_render_device, longest-
-first measured tile schedule of its own layout); --tiles: the cost-balanced tile lists of
-multigpu.balanced_tiles over the whole frame's measured wave times (rt_render_tiles_device, what
-bench.py --gpus N runs by default), each timed with HIP events on the launch stream."""
+first measured tile schedule of its own layout); --tiles: multigpu.rank_plans over the whole
+frame's measured wave times -- a serpentine deal by cost, or with --cut the contiguous runs of
+equal cost (bench.py --gpus N's default) -- with the tiles above H x a rank's per-slot share split
+per sample (or per pixel) on a side stream; every rank's plan timed with HIP events on its stream."""
 import sys
 from pathlib import Path
 
