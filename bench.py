@@ -235,6 +235,7 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
 
+    import numpy as np
     import torch
 
     from distraytracer_old_amd import multigpu, rt, scenes
@@ -274,18 +275,55 @@ def main():
         multigpu.build_photons_sharded(scene, seed, info["photon_count"], dist, device=coll_dev)
         torch.cuda.synchronize()
         photon_s = time.perf_counter() - t
-    # the exchanged frame is the reference's output, ARGB ints (rndrdImg.pixels): 4 bytes a pixel
-    rr = multigpu.RankRenderer(scene, W, H, spp, seed, dist, stage_host=(args.backend == "gloo"), planes=("argb",),
-                               partition=args.partition)
-    r0, r1, rstep, band = rr.rows
+    # the exchanged frame is the reference's output, ARGB ints (rndrdImg.pixels): 4 bytes a pixel.
+    # The N-rank step is the native group (rt_group_*, csrc/group.hip): rank 0 measures the layout's
+    # wave times and broadcasts them, every rank derives the same plan, renders its part, packs it and
+    # sends it to rank 0 over RCCL (ncclSend / ncclRecv), rank 0 scatters it into the frame -- one C
+    # call per frame. N = 1: a one-rank group (every tile, no exchange). --backend gloo (ranks
+    # sharing one GPU, where RCCL cannot run) rehearses the Python path (multigpu.RankRenderer).
+    native = not (world > 1 and args.backend == "gloo")
+    p_frame = rt.params(W, H, spp=spp, seed=seed)
+    if native:
+        if world > 1:
+            uid = torch.zeros(128, dtype=torch.uint8, device=coll_dev)
+            if rank == 0:
+                uid.copy_(torch.frombuffer(bytearray(rt.group_unique_id()), dtype=torch.uint8))
+            dist.broadcast(uid, 0)
+            grp = rt.Group.create_rank(scene, rank, world, bytes(uid.cpu().numpy().tobytes()), W, H, spp=spp,
+                                       seed=seed)
+        else:
+            grp = rt.Group.create([scene], W, H, spp=spp, seed=seed)
+        run_t, split_t = grp.rank_tiles(rank)
+        my_tiles = np.concatenate([run_t, split_t]).astype(np.int32)
+        parallelism = ("1 GPU" if world == 1 else
+                       f"cost-balanced wave tiles over {world} ranks (native rt_group, one process per GPU) "
+                       "+ RCCL send/recv of the ARGB pixels to rank 0")
+
+        def step(ev=None):
+            grp.render()
+
+        def drain():
+            grp.sync()
+    else:
+        rr = multigpu.RankRenderer(scene, W, H, spp, seed, dist, stage_host=True, planes=("argb",),
+                                   partition=args.partition)
+        my_tiles = (np.concatenate([rr.plan.tiles, rr.plan.split]).astype(np.int32)
+                    if rr.partition == "tiles" else None)
+        parallelism = (f"cost-balanced wave tiles over {world} ranks" if rr.partition == "tiles" else
+                       f"{multigpu.BAND}-row bands interleaved over {world} ranks") + " + gloo gather of the ARGB pixels"
+        step, drain = rr.step, rr.finish
 
     # exact per-frame counters (instrumented runs, outside the timed region): the kernel as it
     # runs (top-level culling on: the record loads it issues) and the reference algorithm's work
-    # (RT_RENDER_NOCULL: every objList entry tested for every ray, SURVEY 8(d)'s per-ray bytes)
-    if rr.partition == "tiles":
-        st = scene.render_tiles_count(rr.p, rr.tiles)
-        sr = scene.render_tiles_count(rt.params(W, H, spp=spp, seed=seed, flags=rt.RENDER_NOCULL), rr.tiles)
+    # (RT_RENDER_NOCULL: every objList entry tested for every ray, SURVEY 8(d)'s per-ray bytes).
+    # A rank's split tiles are counted as tile waves (their samples and rays are the same).
+    p_nocull = rt.params(W, H, spp=spp, seed=seed, flags=rt.RENDER_NOCULL)
+    if my_tiles is not None:
+        zero = dict.fromkeys(rt.ST_NAMES, 0)
+        st = scene.render_tiles_count(p_frame, my_tiles) if len(my_tiles) else zero
+        sr = scene.render_tiles_count(p_nocull, my_tiles) if len(my_tiles) else zero
     else:
+        r0, r1, rstep, band = rr.rows
         _, _, st = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=rstep, row_band=band)
         _, _, sr = scene.render_count(W, H, spp=spp, seed=seed, rows=(r0, r1), row_step=rstep, row_band=band,
                                       flags=rt.RENDER_NOCULL)
@@ -294,43 +332,47 @@ def main():
     if dist:
         dist.all_reduce(counts)
     rays_frame, bytes_frame, cam_frame, wbytes_frame, xbytes_frame = [float(x) for x in counts.tolist()]
+    assert int(cam_frame) == W * H * spp, f"counted {cam_frame} camera samples, the frame has {W * H * spp}"
     my_bytes = float(algorithmic_bytes(sr))
     my_xbytes = float(algorithmic_bytes(st))
     my_wbytes = float(wave_bytes(st))
 
-    # setup (untimed, like the counting run): a layout's first two renders calibrate its tile
-    # dispatch order (probe, then measured wave times; rt_render_device in include/distraytracer.h)
-    rr.calibrate()
-    # ... then ~0.2 s of untimed frames: the GPU's clocks ramp over the first few launches
+    # setup (untimed, like the counting run): a layout's calibration renders ran when the group /
+    # renderer was made; ~0.2 s of untimed frames next -- the GPU's clocks ramp over the first launches
     t_warm = time.perf_counter()
     while time.perf_counter() - t_warm < 0.2:
-        rr.render()
-        torch.cuda.synchronize()
+        step()
+        drain()
     for _ in range(args.warmup):
-        rr.step()
-    rr.finish()
+        step()
+    drain()
     torch.cuda.synchronize()
+    if native:
+        grp.kernel_ms(rank)  # reset the kernel-time window
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        rr.step(evs[i])
-    rr.finish()  # the last frame's gather + assemble are inside the timed region
+        step(evs[i])
+    drain()  # the last frame's exchange + scatter are inside the timed region
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    if native:  # HIP events on the rank's render stream (rt_group_kernel_ms)
+        kern_ms, nfr = grp.kernel_ms(rank)
+        assert nfr == min(args.steps, 64), (nfr, args.steps)
+    else:
+        kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
 
     # the drop-in path's cost (rank 0 of a 1-GPU run): rt_render of the whole frame into a host ARGB
     # buffer -- what the JNI draw() does: launch + the 4 B/pixel read-back to
     # pageable host memory, blocking. Timed apart from the steps, after them.
     host_ms = None
     if world == 1:
-        import numpy as np
         px = np.zeros((H, W), dtype=np.int32)
         for _ in range(2):  # this layout's tile-schedule calibration (probe order, then measured order)
             scene.render_argb_into(px, W, H, spp=spp, seed=seed)
@@ -352,14 +394,16 @@ def main():
         achieved_lane = my_bytes / (kern_ms / 1e3) / 1e9
         achieved_lane_x = my_xbytes / (kern_ms / 1e3) / 1e9
         workload = f"{args.config} {cli} {W}x{H} {spp}spp"
+        var_t, var_c = scene.variant()  # the timed and counted render_kernel<CNT, F> instances (same F)
         bid = rt.build_id()
         pmc, tsrc, why = find_pmc(workload, bid, kern_ms) if world == 1 else (None, None, "N > 1")
-        traffic = traffic_rd = traffic_wr = None
+        traffic = traffic_rd = traffic_wr = traffic_lo = None
         fp64 = None
         if pmc:
             traffic_rd = float(pmc["hbm_bytes_per_launch"])
             traffic_wr = pmc.get("hbm_write_bytes_per_launch")
             traffic = traffic_rd + float(traffic_wr or 0)
+            traffic_lo = traffic_rd / 2 + float(traffic_wr or 0)
             if pmc.get("fp64_flop_per_launch"):
                 tf = float(pmc["fp64_flop_per_launch"]) / (kern_ms / 1e3) / 1e12
                 fp64 = {"tflops": tf, "peak_tflops_measured": FP64_PEAK_TFLOPS, "frac": tf / FP64_PEAK_TFLOPS,
@@ -383,10 +427,7 @@ def main():
                     f"scene scenes/{cli} (SURVEY 8(d) {args.config}); synthetic inputs where the reference's are missing",
             "config": {"workload": workload, "width": W, "height": H, "spp": spp, "seed": seed,
                        "rays_per_frame": int(rays_frame), "camera_samples": int(cam_frame),
-                       "parallelism": ("1 GPU" if world == 1 else
-                                       (f"cost-balanced wave tiles over {world} ranks" if rr.partition == "tiles" else
-                                        f"{multigpu.BAND}-row bands interleaved over {world} ranks") +
-                                       f" + {args.backend} gather of the ARGB pixels to rank 0")},
+                       "parallelism": parallelism},
             "camera_msamples_per_s": cam_frame / (ms_per_step / 1e3) / 1e6,
             "kernel_ms_max_over_ranks": kern_ms_max,
             "host_path_ms_per_step": host_ms,
@@ -404,10 +445,18 @@ def main():
                          "traffic_source": tsrc, "traffic_build_id": pmc.get("build_id") if pmc else None,
                          "traffic_kernel_ms": (pmc.get("derived") or {}).get("kernel_ms") if pmc else None,
                          "traffic_missing": why,
-                         "kernel": "render_kernel", "kernel_ms": kern_ms,
+                         "traffic_lower_bound": traffic_lo,
+                         "traffic_note": "L2-to-fabric request bytes (FETCH_SIZE x 2 + WRITE_SIZE x 1, "
+                                         "MI355X_MICROARCH.md HBM section): Infinity-Cache hits are counted, and the "
+                                         "x2 is the guide's rule for 16-B/lane streaming reads while this kernel "
+                                         "reads mostly through scalar and 8-B loads -- an upper bound on HBM bytes; "
+                                         "traffic_lower_bound takes FETCH_SIZE x 1",
+                         "kernel": f"render_kernel<false, {var_t}u>", "kernel_ms": kern_ms,
+                         "counted_kernel": f"render_kernel<true, {var_c}u>",
                          "bytes_per_launch": my_wbytes, "bytes_per_ray": wbytes_frame / max(1.0, rays_frame),
                          "accounting": "8(d) record sizes x record loads per wave step (packet / wave-uniform "
-                                       "records) or per lane (texels)",
+                                       "records) or per lane (texels), counted by counted_kernel: the "
+                                       "instrumented instance of the timed kernel's variant",
                          # SURVEY 8(d) per lane, the reference algorithm's work (nothing culled): bytes
                          # the lanes consume, mostly served by the scalar cache / L2 (a wave loads a
                          # record once for all its lanes) -- a rate, not a fraction of HBM peak
@@ -427,6 +476,8 @@ def main():
             out["cpu_baseline"] = cb
         assert out["n_gpus"] == args.gpus
         print(json.dumps(out), flush=True)
+    if native:
+        grp.close()
     scene.close()
     if dist:
         dist.destroy_process_group()

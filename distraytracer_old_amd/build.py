@@ -24,12 +24,13 @@ LIB_PATH = LIB_DIR / "libdistraytracer.so"
 INFO_PATH = LIB_DIR / "libdistraytracer.buildinfo.json"
 PUBLIC_HEADER = PKG.parent / "include" / "distraytracer.h"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["trace.hip", "render_minreg.hip", "photon_build.hip", "cli_loader.cpp", "scene_build.cpp", "photon.cpp"]
+SOURCES = ["trace.hip", "render_minreg.hip", "photon_build.hip", "group.hip", "cli_loader.cpp", "scene_build.cpp", "photon.cpp"]
 # per-source compiler flags: render_minreg.hip holds C3's and C5's render variants, which run
 # faster with the register-minimising scheduler (C4's variant, in trace.hip, runs slower with it)
 SOURCE_FLAGS = {"render_minreg.hip": ["-Xarch_device", "-mllvm=--amdgpu-sched-strategy=iterative-minreg",
                                       "-Xarch_device", "-mllvm=--amdgpu-use-amdgpu-trackers=1"]}
-HEADERS = ["rt_types.h", "rt_internal.h", "host_math.h", "trace_device.h", "trace_kernels.h", "qdiv.h", "jfdlibm.h"]
+HEADERS = ["rt_types.h", "rt_internal.h", "host_math.h", "trace_device.h", "trace_kernels.h", "wavefront.h", "qdiv.h",
+           "jfdlibm.h"]
 # -ffp-contract=off: keep the reference's (Java) unfused double arithmetic so discrete
 # decisions (hits, shadows, TIR) match the oracle; no fast-math (IEEE Inf/NaN needed).
 COMPILE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
@@ -102,7 +103,7 @@ def build(force: bool = False, verbose: bool = False, defines: list[str] | None 
             failed = f"hipcc failed on {src}:\n" + err[-4000:]
     if failed:
         raise RuntimeError(failed)
-    r = subprocess.run([HIPCC, "-shared", "--offload-arch=gfx950", "-o", str(tmp), *objs], capture_output=True, text=True)
+    r = subprocess.run([HIPCC, "-shared", "--offload-arch=gfx950", "-o", str(tmp), *objs, "-ldl"], capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n" + r.stderr[-4000:])
     if verbose:

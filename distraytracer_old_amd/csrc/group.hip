@@ -1,0 +1,840 @@
+// Multi-GPU frame behind the C ABI (include/distraytracer.h rt_group_*).
+//
+// The reference renders one image on one thread (myFOVScene.draw, myScene.java:1481-1531); pixels
+// and their samples are independent, so the frame shards by wave tiles. A group is N ranks, one GPU
+// each (or N ranks sharing devices for the one-GPU emulation), each holding the replicated scene:
+//
+//   plan     rank 0's measured wave time of every tile of the whole-frame layout (rt_tile_costs)
+//            cut into N contiguous runs of equal cost; tiles whose own wave would outlast a rank's
+//            share are rendered one sample per wave beside the run (plan_ranks, deterministic, so
+//            every process derives the same plan from the broadcast costs);
+//   step     rank r renders its run (tile list) + split pixels into a whole-frame buffer on its
+//            stream; ranks r > 0 pack their pixels (pack_kernel) and send them to rank 0 over RCCL
+//            (ncclSend / ncclRecv in one group: each rank's pixels cross its own xGMI link into rank
+//            0 once) or, in the one-process emulation, by device copies; rank 0, which rendered its
+//            own run straight into the output frame, scatters the received pixels into it
+//            (scatter_kernel). The exchange runs on a third stream per rank with double-buffered
+//            send / receive slabs, so frame f's exchange overlaps frame f + 1's render.
+//
+// Pixels, their RNG keys and their per-pixel sample order do not depend on the plan, so the frame
+// equals the 1-GPU frame bit for bit for every N and transport.
+//
+// RCCL is loaded at run time (dlopen of librccl.so.1, which in a PyTorch process is the copy torch
+// already loaded), so the library and the COPY transport work without it.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rt_internal.h"
+
+using namespace rt;
+
+#define GCHK(expr)                                                                       \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return set_error(RT_E_HIP, std::string(#expr " failed: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// RCCL, resolved at run time
+namespace {
+struct Rccl {
+  bool tried = false, ok = false;
+  std::string why;
+  decltype(&ncclGetUniqueId) getUniqueId = nullptr;
+  decltype(&ncclCommInitRank) commInitRank = nullptr;
+  decltype(&ncclCommInitAll) commInitAll = nullptr;
+  decltype(&ncclCommDestroy) commDestroy = nullptr;
+  decltype(&ncclGroupStart) groupStart = nullptr;
+  decltype(&ncclGroupEnd) groupEnd = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclBroadcast) bcast = nullptr;
+  decltype(&ncclGetErrorString) errStr = nullptr;
+};
+Rccl g_rccl;
+std::mutex g_rccl_mu;
+
+int rccl_load() {
+  std::lock_guard<std::mutex> lk(g_rccl_mu);
+  Rccl& R = g_rccl;
+  if (!R.tried) {
+    R.tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      R.why = std::string("cannot load librccl.so.1: ") + dlerror();
+    } else {
+      bool all = true;
+      auto sym = [&](auto& fn, const char* name) {
+        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+        all = all && fn != nullptr;
+      };
+      sym(R.getUniqueId, "ncclGetUniqueId");
+      sym(R.commInitRank, "ncclCommInitRank");
+      sym(R.commInitAll, "ncclCommInitAll");
+      sym(R.commDestroy, "ncclCommDestroy");
+      sym(R.groupStart, "ncclGroupStart");
+      sym(R.groupEnd, "ncclGroupEnd");
+      sym(R.send, "ncclSend");
+      sym(R.recv, "ncclRecv");
+      sym(R.bcast, "ncclBroadcast");
+      sym(R.errStr, "ncclGetErrorString");
+      R.ok = all;
+      if (!all) R.why = "librccl.so.1 lacks an entry point the group needs";
+    }
+  }
+  return R.ok ? RT_OK : set_error(RT_E_INVALID, "RCCL transport unavailable: " + R.why);
+}
+
+#define NCHK(expr)                                                                                   \
+  do {                                                                                               \
+    ncclResult_t r_ = (expr);                                                                        \
+    if (r_ != ncclSuccess)                                                                           \
+      return set_error(RT_E_HIP, std::string(#expr " failed: ") + g_rccl.errStr(r_));               \
+  } while (0)
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// plan (host only; multigpu.py rank_plans is the independent Python restatement the tests compare)
+namespace rt {
+// owner[t]: rank in [0, world) rendering tile t in its wave run, or world + rank when the tile is
+// one of that rank's split (one sample per wave) tiles. order: every tile in dispatch order --
+// longest first by quarter-octave cost bucket, row-major inside a bucket; a rank's run and split
+// tiles are the subsequences of `order` it owns.
+void plan_ranks(const uint32_t* cost, int n, int world, double heavy, int slots, int32_t* owner, int32_t* order) {
+  // contiguous cut: tile t goes to the rank holding its cost midpoint (prefix sums of integer costs,
+  // exact in double for < 2^53)
+  double total = 0;
+  for (int t = 0; t < n; ++t) total += (double)cost[t];
+  double cum = 0;
+  for (int t = 0; t < n; ++t) {
+    const double c = (double)cost[t];
+    cum += c;
+    int r;
+    if (total > 0) {
+      const double mid = cum - 0.5 * c;
+      const double q = (mid * world) / total;
+      r = (int)std::min<int64_t>((int64_t)q, world - 1);
+    } else {
+      r = (int)((int64_t)t * world / std::max(1, n));
+    }
+    owner[t] = r;
+  }
+  // heavy tiles: a wave longer than `heavy` x a rank's ideal per-slot share is split per sample
+  if (world > 1) {
+    const double thr = heavy * total / ((double)slots * world);
+    for (int t = 0; t < n; ++t)
+      if ((double)cost[t] > thr) owner[t] += world;
+  }
+  // dispatch order: counting sort by bucket, longest first, stable (row-major inside a bucket)
+  constexpr int NB = 4 * 32 + 1;
+  std::vector<int> start(NB, 0);
+  std::vector<uint8_t> key(n);
+  for (int t = 0; t < n; ++t) {
+    key[t] = (uint8_t)cost_bucket(cost[t]);
+    start[key[t]]++;
+  }
+  for (int k = NB - 1, acc = 0; k >= 0; --k) {
+    const int h = start[k];
+    start[k] = acc;
+    acc += h;
+  }
+  for (int t = 0; t < n; ++t) order[start[key[t]]++] = t;
+}
+}  // namespace rt
+
+// ---------------------------------------------------------------------------------------------
+// pack / scatter kernels (ARGB int32 and the optional float-RGB plane)
+__global__ void __launch_bounds__(256) pack_kernel(const int32_t* __restrict__ argb, const float* __restrict__ rgb,
+                                                   const int32_t* __restrict__ idx, int n, int32_t* __restrict__ oa,
+                                                   float* __restrict__ orgb) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t p = idx[i];
+  oa[i] = argb[p];
+  if (orgb) {
+    orgb[3 * (int64_t)i + 0] = rgb[3 * p + 0];
+    orgb[3 * (int64_t)i + 1] = rgb[3 * p + 1];
+    orgb[3 * (int64_t)i + 2] = rgb[3 * p + 2];
+  }
+}
+__global__ void __launch_bounds__(256) scatter_kernel(const int32_t* __restrict__ ia, const float* __restrict__ irgb,
+                                                      const int32_t* __restrict__ idx, int n, int32_t* __restrict__ argb,
+                                                      float* __restrict__ rgb) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t p = idx[i];
+  argb[p] = ia[i];
+  if (rgb) {
+    rgb[3 * p + 0] = irgb[3 * (int64_t)i + 0];
+    rgb[3 * p + 1] = irgb[3 * (int64_t)i + 1];
+    rgb[3 * p + 2] = irgb[3 * (int64_t)i + 2];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+namespace {
+constexpr int KRING = 64;  // frames of kernel-time events kept per rank
+
+struct GRank {
+  rt_scene* s = nullptr;
+  int dev = 0, rank = 0;
+  hipStream_t st = nullptr, side = nullptr, cs = nullptr;  // render, split pixels, exchange
+  ParamsD P{};
+  std::vector<int32_t> hTiles, hSplit, hPix, hAll;  // run tiles, split tiles, split pixels, every pixel written
+  int32_t *dTiles = nullptr, *dPix = nullptr, *dAll = nullptr;
+  double* smpCol = nullptr;
+  uint8_t* smpTr = nullptr;
+  float* fRgb = nullptr;  // whole-frame render target (ranks > 0)
+  int32_t* fArgb = nullptr;
+  float* sRgb[2] = {};
+  int32_t* sArgb[2] = {};
+  hipEvent_t evStart = nullptr, evSide = nullptr, evPacked = nullptr, evSent[2] = {}, evRendered = nullptr;
+  hipEvent_t tA[KRING] = {}, tB[KRING] = {};
+  int64_t timed = 0;  // frames with kernel events since the last rt_group_kernel_ms
+  ncclComm_t comm = nullptr;
+  int64_t off = 0;  // offset of this rank's pixels in rank 0's receive slab
+};
+}  // namespace
+
+struct rt_group {
+  int world = 1;
+  bool rankMode = false, useRccl = false, rgb = false, root = false;
+  uint32_t renderFlags = 0;
+  rt_render_params p{};
+  int W = 0, H = 0, ntiles = 0, tilesX = 0, tw = 0, th = 0;
+  std::vector<int32_t> owner, order;
+  std::vector<int64_t> npix;   // pixels written per rank
+  std::vector<GRank> r;        // the ranks this process drives (all of them in local mode)
+  // rank 0 (root) state
+  int rootDev = 0;
+  int64_t nRecv = 0;
+  int32_t* dScat = nullptr;     // pixels of ranks 1.. in receive-slab order
+  float* rRgb[2] = {};
+  int32_t* rArgb[2] = {};
+  float* outRgb = nullptr;      // internal frame (rt_group_render with NULL outputs, rt_group_render_host)
+  int32_t* outArgb = nullptr;
+  void* stage = nullptr;        // pinned read-back staging (rt_group_render_host)
+  hipEvent_t evRecv[2] = {};    // receive slab b consumed by its scatter
+  std::vector<hipEvent_t> evCopied;  // COPY transport: rank r's copy into the slab done
+  int64_t frame = 0;
+  std::vector<void*> allocs;
+};
+
+namespace {
+int gmalloc(rt_group* g, void** p, size_t bytes) {
+  *p = nullptr;
+  if (bytes == 0) return RT_OK;
+  GCHK(hipMalloc(p, bytes));
+  g->allocs.push_back(*p);
+  return RT_OK;
+}
+template <class T>
+int gupload(rt_group* g, const std::vector<T>& v, T** out) {
+  int rc = gmalloc(g, (void**)out, v.size() * sizeof(T));
+  if (rc || v.empty()) return rc;
+  GCHK(hipMemcpy(*out, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+// pixels (row * W + col) of tile t of the whole-frame layout, row-major inside the tile, clipped
+void tile_pixels(const rt_group* g, int t, std::vector<int32_t>& out) {
+  const int tx = t % g->tilesX, ty = t / g->tilesX;
+  for (int dy = 0; dy < g->th; ++dy)
+    for (int dx = 0; dx < g->tw; ++dx) {
+      const int row = ty * g->th + dy, col = tx * g->tw + dx;
+      if (row < g->H && col < g->W) out.push_back(row * g->W + col);
+    }
+}
+
+// host lists of rank q from the plan
+void rank_lists(const rt_group* g, int q, std::vector<int32_t>& tiles, std::vector<int32_t>& split,
+                std::vector<int32_t>& pix, std::vector<int32_t>& all) {
+  tiles.clear(); split.clear(); pix.clear(); all.clear();
+  for (int t : g->order) {
+    if (g->owner[t] == q) tiles.push_back(t);
+    else if (g->owner[t] == g->world + q) split.push_back(t);
+  }
+  for (int t : split) tile_pixels(g, t, pix);
+  for (int t : tiles) tile_pixels(g, t, all);
+  all.insert(all.end(), pix.begin(), pix.end());
+}
+
+int destroy_group(rt_group* g);
+
+// everything after the plan: per-rank buffers, streams, events, lists; root slabs
+int setup_ranks(rt_group* g) {
+  g->npix.assign(g->world, 0);
+  {
+    std::vector<int32_t> a, b, c, d;
+    for (int q = 0; q < g->world; ++q) {
+      rank_lists(g, q, a, b, c, d);
+      g->npix[q] = (int64_t)d.size();
+    }
+  }
+  int64_t off = 0;
+  std::vector<int64_t> offs(g->world, 0);
+  for (int q = 1; q < g->world; ++q) { offs[q] = off; off += g->npix[q]; }
+  g->nRecv = off;
+  const size_t npx = (size_t)g->W * g->H;
+  for (GRank& R : g->r) {
+    GCHK(hipSetDevice(R.dev));
+    int rc;
+    if ((rc = prepare_render(R.s, &g->p, R.P))) return rc;
+    rank_lists(g, R.rank, R.hTiles, R.hSplit, R.hPix, R.hAll);
+    R.off = offs[R.rank];
+    GCHK(hipStreamCreateWithFlags(&R.st, hipStreamNonBlocking));
+    GCHK(hipStreamCreateWithFlags(&R.side, hipStreamNonBlocking));
+    GCHK(hipStreamCreateWithFlags(&R.cs, hipStreamNonBlocking));
+    GCHK(hipEventCreateWithFlags(&R.evStart, hipEventDisableTiming));
+    GCHK(hipEventCreateWithFlags(&R.evSide, hipEventDisableTiming));
+    GCHK(hipEventCreateWithFlags(&R.evPacked, hipEventDisableTiming));
+    GCHK(hipEventCreateWithFlags(&R.evRendered, hipEventDisableTiming));
+    for (int b = 0; b < 2; ++b) GCHK(hipEventCreateWithFlags(&R.evSent[b], hipEventDisableTiming));
+    for (int k = 0; k < KRING; ++k) {
+      GCHK(hipEventCreate(&R.tA[k]));
+      GCHK(hipEventCreate(&R.tB[k]));
+    }
+    if ((rc = gupload(g, R.hTiles, &R.dTiles)) || (rc = gupload(g, R.hPix, &R.dPix)) || (rc = gupload(g, R.hAll, &R.dAll)))
+      return rc;
+    const size_t ns = R.hPix.size() * (size_t)R.P.spp;
+    if ((rc = gmalloc(g, (void**)&R.smpCol, ns * 3 * sizeof(double))) || (rc = gmalloc(g, (void**)&R.smpTr, ns))) return rc;
+    if (R.rank != 0) {
+      if ((rc = gmalloc(g, (void**)&R.fArgb, npx * sizeof(int32_t)))) return rc;
+      if (g->rgb && (rc = gmalloc(g, (void**)&R.fRgb, npx * 3 * sizeof(float)))) return rc;
+      for (int b = 0; b < 2; ++b) {
+        if ((rc = gmalloc(g, (void**)&R.sArgb[b], R.hAll.size() * sizeof(int32_t)))) return rc;
+        if (g->rgb && (rc = gmalloc(g, (void**)&R.sRgb[b], R.hAll.size() * 3 * sizeof(float)))) return rc;
+      }
+    }
+  }
+  if (g->root) {
+    GCHK(hipSetDevice(g->rootDev));
+    std::vector<int32_t> scat;
+    scat.reserve(g->nRecv);
+    std::vector<int32_t> a, b, c, d;
+    for (int q = 1; q < g->world; ++q) {
+      rank_lists(g, q, a, b, c, d);
+      scat.insert(scat.end(), d.begin(), d.end());
+    }
+    int rc;
+    if ((rc = gupload(g, scat, &g->dScat))) return rc;
+    for (int b2 = 0; b2 < 2; ++b2) {
+      if ((rc = gmalloc(g, (void**)&g->rArgb[b2], g->nRecv * sizeof(int32_t)))) return rc;
+      if (g->rgb && (rc = gmalloc(g, (void**)&g->rRgb[b2], g->nRecv * 3 * sizeof(float)))) return rc;
+      GCHK(hipEventCreateWithFlags(&g->evRecv[b2], hipEventDisableTiming));
+    }
+    if ((rc = gmalloc(g, (void**)&g->outArgb, npx * sizeof(int32_t)))) return rc;
+    if (g->rgb && (rc = gmalloc(g, (void**)&g->outRgb, npx * 3 * sizeof(float)))) return rc;
+    if (!g->useRccl) {
+      g->evCopied.assign(g->world, nullptr);
+      for (int q = 0; q < g->world; ++q) GCHK(hipEventCreateWithFlags(&g->evCopied[q], hipEventDisableTiming));
+    }
+  }
+  return RT_OK;
+}
+
+int make_layout(rt_group* g, rt_scene* s, const rt_render_params* p, uint32_t flags) {
+  if (!p) return set_error(RT_E_INVALID, "rt_group: null params");
+  if (p->flags & (RT_RENDER_WAVEFRONT | RT_RENDER_PIXEL_WAVES))
+    return set_error(RT_E_INVALID, "rt_group: RT_RENDER_WAVEFRONT / RT_RENDER_PIXEL_WAVES are not group layouts");
+  g->p = *p;
+  g->p.row0 = 0; g->p.row1 = p->height; g->p.row_step = 1; g->p.row_band = 1;
+  g->p.flags = p->flags & ~(uint32_t)RT_RENDER_ROWMAJOR;
+  g->rgb = (flags & RT_GROUP_RGB) != 0;
+  g->W = p->width;
+  g->H = p->height;
+  ParamsD P{};
+  int rc = prepare_render(s, &g->p, P);
+  if (rc) return rc;
+  const int ncols = P.W;
+  g->tw = P.tw; g->th = P.th;
+  g->tilesX = (ncols + P.tw - 1) / P.tw;
+  g->ntiles = g->tilesX * ((P.nrows + P.th - 1) / P.th);
+  return RT_OK;
+}
+
+int make_plan(rt_group* g, const std::vector<uint32_t>& cost, double heavy, int slots) {
+  if (!(heavy > 0)) heavy = 1.25;
+  if (slots <= 0) slots = 4096;
+  g->owner.assign(g->ntiles, 0);
+  g->order.assign(g->ntiles, 0);
+  plan_ranks(cost.data(), g->ntiles, g->world, heavy, slots, g->owner.data(), g->order.data());
+  return RT_OK;
+}
+
+GRank* local_rank(rt_group* g, int rank) {
+  for (GRank& R : g->r)
+    if (R.rank == rank) return &R;
+  return nullptr;
+}
+
+// rank R's render of the frame into (rgb, argb) on R.st (split pixels on R.side beside it)
+int enqueue_render(rt_group* g, GRank& R, float* rgb, int32_t* argb, bool timed) {
+  GCHK(hipSetDevice(R.dev));
+  if (timed) GCHK(hipEventRecord(R.tA[R.timed % KRING], R.st));
+  int rc;
+  if (!R.hPix.empty()) {
+    GCHK(hipEventRecord(R.evStart, R.st));
+    GCHK(hipStreamWaitEvent(R.side, R.evStart, 0));
+    if ((rc = launch_pixel_list(R.s, R.P, g->p.flags, R.dPix, (int)R.hPix.size(), R.smpCol, R.smpTr, rgb, argb, R.side)))
+      return rc;
+    GCHK(hipEventRecord(R.evSide, R.side));
+  }
+  if (!R.hTiles.empty() && (rc = launch_tile_list(R.s, R.P, g->p.flags, R.dTiles, (int)R.hTiles.size(), rgb, argb, R.st)))
+    return rc;
+  if (!R.hPix.empty()) GCHK(hipStreamWaitEvent(R.st, R.evSide, 0));
+  if (timed) {
+    GCHK(hipEventRecord(R.tB[R.timed % KRING], R.st));
+    R.timed++;
+  }
+  return RT_OK;
+}
+
+// rank R (> 0): pack its pixels of frame buffer b's send slab (after the send that last used it)
+int enqueue_pack(rt_group* g, GRank& R, int b) {
+  const int n = (int)R.hAll.size();
+  if (n == 0) return RT_OK;
+  GCHK(hipStreamWaitEvent(R.st, R.evSent[b], 0));
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, R.st, R.fArgb, R.fRgb, R.dAll, n,
+                     R.sArgb[b], g->rgb ? R.sRgb[b] : nullptr);
+  GCHK(hipGetLastError());
+  GCHK(hipEventRecord(R.evPacked, R.st));
+  GCHK(hipStreamWaitEvent(R.cs, R.evPacked, 0));
+  return RT_OK;
+}
+
+// root: scatter receive slab b (pixels [lo, hi) of it) into the frame on stream cs
+int enqueue_scatter(rt_group* g, hipStream_t cs, int b, int64_t lo, int64_t hi, float* rgb, int32_t* argb) {
+  const int n = (int)(hi - lo);
+  if (n <= 0) return RT_OK;
+  hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, cs, g->rArgb[b] + lo,
+                     g->rgb ? g->rRgb[b] + 3 * lo : nullptr, g->dScat + lo, n, argb, g->rgb ? rgb : nullptr);
+  GCHK(hipGetLastError());
+  return RT_OK;
+}
+
+// one frame; rgb / argb: rank 0's output frame on its device (NULL: the internal frame)
+int group_frame(rt_group* g, float* rgb, int32_t* argb) {
+  const int b = (int)(g->frame & 1);
+  if (g->root) {
+    if (!argb) argb = g->outArgb;
+    if (!rgb) rgb = g->outRgb;
+    if (rgb && !g->rgb) return set_error(RT_E_INVALID, "rt_group: float-RGB output needs RT_GROUP_RGB");
+  }
+  int rc;
+  // renders (+ packs) of every local rank
+  for (GRank& R : g->r) {
+    const bool r0 = R.rank == 0;
+    if ((rc = enqueue_render(g, R, r0 ? rgb : R.fRgb, r0 ? argb : R.fArgb, true))) return rc;
+    if (!r0 && g->world > 1 && (rc = enqueue_pack(g, R, b))) return rc;
+  }
+  GRank* R0 = g->root ? local_rank(g, 0) : nullptr;
+  if (g->world > 1) {
+    if (g->useRccl) {
+      // the single exchange: ranks > 0 send their packed pixels to rank 0 (grouped point-to-point)
+      if (R0) {
+        GCHK(hipSetDevice(R0->dev));
+        GCHK(hipStreamWaitEvent(R0->cs, g->evRecv[b], 0));
+      }
+      NCHK(g_rccl.groupStart());
+      for (GRank& R : g->r) {
+        const size_t n = R.hAll.size();
+        if (R.rank != 0 && n) {
+          NCHK(g_rccl.send(R.sArgb[b], n, ncclInt32, 0, R.comm, R.cs));
+          if (g->rgb) NCHK(g_rccl.send(R.sRgb[b], 3 * n, ncclFloat32, 0, R.comm, R.cs));
+        }
+      }
+      if (R0)
+        for (int q = 1; q < g->world; ++q) {
+          int64_t o = 0;
+          for (int k = 1; k < q; ++k) o += g->npix[k];
+          const size_t n = (size_t)g->npix[q];
+          if (!n) continue;
+          NCHK(g_rccl.recv(g->rArgb[b] + o, n, ncclInt32, q, R0->comm, R0->cs));
+          if (g->rgb) NCHK(g_rccl.recv(g->rRgb[b] + 3 * o, 3 * n, ncclFloat32, q, R0->comm, R0->cs));
+        }
+      NCHK(g_rccl.groupEnd());
+      for (GRank& R : g->r)
+        if (R.rank != 0) {
+          GCHK(hipSetDevice(R.dev));
+          GCHK(hipEventRecord(R.evSent[b], R.cs));
+        }
+    } else {
+      // one process: device copies of every rank's packed pixels into rank 0's receive slab
+      GCHK(hipSetDevice(R0->dev));
+      for (GRank& R : g->r) {
+        const size_t n = R.hAll.size();
+        if (R.rank == 0) continue;
+        GCHK(hipSetDevice(R.dev));
+        GCHK(hipStreamWaitEvent(R.cs, g->evRecv[b], 0));
+        if (n) {
+          GCHK(hipMemcpyPeerAsync(g->rArgb[b] + R.off, g->rootDev, R.sArgb[b], R.dev, n * sizeof(int32_t), R.cs));
+          if (g->rgb)
+            GCHK(hipMemcpyPeerAsync(g->rRgb[b] + 3 * R.off, g->rootDev, R.sRgb[b], R.dev, n * 3 * sizeof(float), R.cs));
+        }
+        GCHK(hipEventRecord(R.evSent[b], R.cs));
+        GCHK(hipEventRecord(g->evCopied[R.rank], R.cs));
+      }
+      GCHK(hipSetDevice(R0->dev));
+      for (GRank& R : g->r)
+        if (R.rank != 0) GCHK(hipStreamWaitEvent(R0->cs, g->evCopied[R.rank], 0));
+    }
+    if (R0) {
+      GCHK(hipSetDevice(R0->dev));
+      if ((rc = enqueue_scatter(g, R0->cs, b, 0, g->nRecv, rgb, argb))) return rc;
+      GCHK(hipEventRecord(g->evRecv[b], R0->cs));
+    }
+  }
+  if (R0) {  // the frame is complete when rank 0's own render and the scatter are
+    GCHK(hipSetDevice(R0->dev));
+    GCHK(hipEventRecord(R0->evRendered, R0->st));
+    GCHK(hipStreamWaitEvent(R0->cs, R0->evRendered, 0));
+  }
+  g->frame++;
+  return RT_OK;
+}
+
+int sync_group(rt_group* g) {
+  for (GRank& R : g->r) {
+    GCHK(hipSetDevice(R.dev));
+    GCHK(hipStreamSynchronize(R.side));
+    GCHK(hipStreamSynchronize(R.st));
+    GCHK(hipStreamSynchronize(R.cs));
+  }
+  return RT_OK;
+}
+
+int destroy_group(rt_group* g) {
+  if (!g) return RT_OK;
+  for (GRank& R : g->r) {
+    (void)hipSetDevice(R.dev);
+    if (R.side) (void)hipStreamSynchronize(R.side);
+    if (R.st) (void)hipStreamSynchronize(R.st);
+    if (R.cs) (void)hipStreamSynchronize(R.cs);
+  }
+  for (GRank& R : g->r) {
+    (void)hipSetDevice(R.dev);
+    if (R.comm && g_rccl.ok) (void)g_rccl.commDestroy(R.comm);
+    for (hipEvent_t e : {R.evStart, R.evSide, R.evPacked, R.evRendered, R.evSent[0], R.evSent[1]})
+      if (e) (void)hipEventDestroy(e);
+    for (int k = 0; k < KRING; ++k) {
+      if (R.tA[k]) (void)hipEventDestroy(R.tA[k]);
+      if (R.tB[k]) (void)hipEventDestroy(R.tB[k]);
+    }
+    if (R.st) (void)hipStreamDestroy(R.st);
+    if (R.side) (void)hipStreamDestroy(R.side);
+    if (R.cs) (void)hipStreamDestroy(R.cs);
+  }
+  for (hipEvent_t e : g->evCopied)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : g->evRecv)
+    if (e) (void)hipEventDestroy(e);
+  for (void* p : g->allocs) (void)hipFree(p);
+  if (g->stage) (void)hipHostFree(g->stage);
+  delete g;
+  return RT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rt_rank_plan(const uint32_t* cost, int ntiles, int world, double heavy, int slots, int32_t* owner, int32_t* order) {
+  if (ntiles < 0 || world < 1 || (ntiles > 0 && (!cost || !owner || !order)))
+    return set_error(RT_E_INVALID, "rt_rank_plan: bad arguments");
+  if (!(heavy > 0)) heavy = 1.25;
+  if (slots <= 0) slots = 4096;
+  plan_ranks(cost, ntiles, world, heavy, slots, owner, order);
+  return RT_OK;
+}
+
+int rt_group_unique_id(void* id, int cap) {
+  if (!id || cap < (int)sizeof(ncclUniqueId)) return set_error(RT_E_INVALID, "rt_group_unique_id: buffer < 128 bytes");
+  int rc = rccl_load();
+  if (rc) return rc;
+  ncclUniqueId u;
+  NCHK(g_rccl.getUniqueId(&u));
+  std::memcpy(id, &u, sizeof(u));
+  return (int)sizeof(u);
+}
+
+int rt_group_create(rt_scene* const* scenes, int n, const rt_render_params* p, uint32_t flags, double heavy, int slots,
+                    rt_group** out) {
+  if (!scenes || n < 1 || !out) return set_error(RT_E_INVALID, "rt_group_create: bad arguments");
+  *out = nullptr;
+  for (int i = 0; i < n; ++i)
+    if (!scenes[i]) return set_error(RT_E_INVALID, "rt_group_create: null scene");
+  const bool rccl = n > 1 && !(flags & RT_GROUP_COPY);
+  if (rccl) {
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < i; ++j)
+        if (scenes[i]->device == scenes[j]->device)
+          return set_error(RT_E_INVALID, "rt_group_create: the RCCL transport needs one device per rank (RT_GROUP_COPY shares)");
+    int rc = rccl_load();
+    if (rc) return rc;
+  }
+  rt_group* g = new rt_group();
+  g->world = n;
+  g->useRccl = rccl;
+  g->root = true;
+  g->rootDev = scenes[0]->device;
+  int rc = make_layout(g, scenes[0], p, flags);
+  std::vector<uint32_t> cost;
+  if (rc == RT_OK) {
+    cost.assign(g->ntiles, 1);
+    const int m = rt_tile_costs(scenes[0], &g->p, cost.data(), g->ntiles);
+    rc = m < 0 ? m : (m != g->ntiles ? set_error(RT_E_INVALID, "rt_group_create: tile count mismatch") : RT_OK);
+  }
+  if (rc == RT_OK) rc = make_plan(g, cost, heavy, slots);
+  if (rc == RT_OK) {
+    g->r.resize(n);
+    for (int i = 0; i < n; ++i) {
+      g->r[i].s = scenes[i];
+      g->r[i].dev = scenes[i]->device;
+      g->r[i].rank = i;
+    }
+    rc = setup_ranks(g);
+  }
+  if (rc == RT_OK && rccl) {
+    std::vector<ncclComm_t> comms(n);
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) devs[i] = g->r[i].dev;
+    ncclResult_t nr = g_rccl.commInitAll(comms.data(), n, devs.data());
+    if (nr != ncclSuccess) rc = set_error(RT_E_HIP, std::string("ncclCommInitAll failed: ") + g_rccl.errStr(nr));
+    else
+      for (int i = 0; i < n; ++i) g->r[i].comm = comms[i];
+  }
+  if (rc != RT_OK) {
+    const std::string msg = rt_last_error();
+    destroy_group(g);
+    return set_error(rc, msg);
+  }
+  *out = g;
+  return RT_OK;
+}
+
+int rt_group_create_rank(rt_scene* scene, int rank, int world, const void* unique_id, const rt_render_params* p,
+                         uint32_t flags, double heavy, int slots, rt_group** out) {
+  if (!scene || !out || world < 1 || rank < 0 || rank >= world || (world > 1 && !unique_id))
+    return set_error(RT_E_INVALID, "rt_group_create_rank: bad arguments");
+  *out = nullptr;
+  if (world > 1) {
+    int rc = rccl_load();
+    if (rc) return rc;
+  }
+  rt_group* g = new rt_group();
+  g->world = world;
+  g->rankMode = true;
+  g->useRccl = world > 1;
+  g->root = rank == 0;
+  g->rootDev = scene->device;
+  int rc = make_layout(g, scene, p, flags);
+  GRank R;
+  R.s = scene;
+  R.dev = scene->device;
+  R.rank = rank;
+  if (rc == RT_OK && world > 1) {
+    ncclUniqueId u;
+    std::memcpy(&u, unique_id, sizeof(u));
+    hipError_t he = hipSetDevice(R.dev);
+    if (he != hipSuccess) rc = set_error(RT_E_HIP, hipGetErrorString(he));
+    ncclResult_t nr = rc ? ncclSuccess : g_rccl.commInitRank(&R.comm, world, u, rank);
+    if (nr != ncclSuccess) rc = set_error(RT_E_HIP, std::string("ncclCommInitRank failed: ") + g_rccl.errStr(nr));
+  }
+  std::vector<uint32_t> cost;
+  if (rc == RT_OK) {  // rank 0 measures the layout's wave times; every rank receives them
+    cost.assign(g->ntiles, 1);
+    if (rank == 0) {
+      const int m = rt_tile_costs(scene, &g->p, cost.data(), g->ntiles);
+      rc = m < 0 ? m : (m != g->ntiles ? set_error(RT_E_INVALID, "rt_group_create_rank: tile count mismatch") : RT_OK);
+    }
+    if (world > 1) {  // (every rank reaches the broadcast: a failed calibration sends unit costs, then reports)
+      uint32_t* d = nullptr;
+      hipStream_t st = nullptr;
+      hipError_t he = hipSetDevice(R.dev);
+      if (he == hipSuccess) he = hipMalloc(&d, sizeof(uint32_t) * g->ntiles);
+      if (he == hipSuccess) he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+      if (he == hipSuccess) he = hipMemcpy(d, cost.data(), sizeof(uint32_t) * g->ntiles, hipMemcpyHostToDevice);
+      ncclResult_t nr = ncclSuccess;
+      if (he == hipSuccess) nr = g_rccl.bcast(d, d, (size_t)g->ntiles, ncclUint32, 0, R.comm, st);
+      if (he == hipSuccess && nr == ncclSuccess) he = hipStreamSynchronize(st);
+      if (he == hipSuccess && nr == ncclSuccess) he = hipMemcpy(cost.data(), d, sizeof(uint32_t) * g->ntiles, hipMemcpyDeviceToHost);
+      if (st) (void)hipStreamDestroy(st);
+      if (d) (void)hipFree(d);
+      if (rc == RT_OK && he != hipSuccess) rc = set_error(RT_E_HIP, std::string("cost broadcast: ") + hipGetErrorString(he));
+      if (rc == RT_OK && nr != ncclSuccess) rc = set_error(RT_E_HIP, std::string("cost broadcast: ") + g_rccl.errStr(nr));
+    }
+  }
+  if (rc == RT_OK) rc = make_plan(g, cost, heavy, slots);
+  if (rc == RT_OK) {
+    g->r.push_back(R);
+    R.comm = nullptr;  // owned by g->r[0] now
+    rc = setup_ranks(g);
+  } else if (R.comm) {
+    (void)g_rccl.commDestroy(R.comm);
+  }
+  if (rc != RT_OK) {
+    const std::string msg = rt_last_error();
+    destroy_group(g);
+    return set_error(rc, msg);
+  }
+  *out = g;
+  return RT_OK;
+}
+
+int rt_group_render(rt_group* g, float* d_rgb, int32_t* d_argb) {
+  if (!g) return set_error(RT_E_INVALID, "rt_group_render: null group");
+  return group_frame(g, d_rgb, d_argb);
+}
+
+int rt_group_sync(rt_group* g) {
+  if (!g) return set_error(RT_E_INVALID, "rt_group_sync: null group");
+  return sync_group(g);
+}
+
+int rt_group_render_host(rt_group* g, float* rgb, int32_t* argb) {
+  if (!g) return set_error(RT_E_INVALID, "rt_group_render_host: null group");
+  if (rgb && !g->rgb) return set_error(RT_E_INVALID, "rt_group_render_host: float-RGB output needs RT_GROUP_RGB");
+  int rc = group_frame(g, g->root ? g->outRgb : nullptr, g->root ? g->outArgb : nullptr);
+  if (rc) return rc;
+  if (!g->root) return sync_group(g);
+  GRank* R0 = local_rank(g, 0);
+  const size_t npx = (size_t)g->W * g->H;
+  const size_t na = argb ? npx * sizeof(int32_t) : 0, nr = rgb ? npx * 3 * sizeof(float) : 0;
+  GCHK(hipSetDevice(R0->dev));
+  if (!g->stage && (na + nr) > 0) GCHK(hipHostMalloc(&g->stage, npx * (sizeof(int32_t) + (g->rgb ? 3 * sizeof(float) : 0))));
+  char* stg = (char*)g->stage;
+  if (argb) GCHK(hipMemcpyAsync(stg, g->outArgb, na, hipMemcpyDeviceToHost, R0->cs));
+  if (rgb) GCHK(hipMemcpyAsync(stg + na, g->outRgb, nr, hipMemcpyDeviceToHost, R0->cs));
+  if ((rc = sync_group(g))) return rc;
+  if (argb) std::memcpy(argb, stg, na);
+  if (rgb) std::memcpy(rgb, stg + na, nr);
+  return RT_OK;
+}
+
+int rt_group_frame(rt_group* g, float** d_rgb, int32_t** d_argb) {
+  if (!g) return set_error(RT_E_INVALID, "rt_group_frame: null group");
+  if (d_rgb) *d_rgb = g->root ? g->outRgb : nullptr;
+  if (d_argb) *d_argb = g->root ? g->outArgb : nullptr;
+  return RT_OK;
+}
+
+int rt_group_info(const rt_group* g, int64_t* info, int n) {
+  if (!g || !info) return set_error(RT_E_INVALID, "rt_group_info: null argument");
+  const int64_t v[9] = {g->world, (int64_t)g->r.size(), g->r.empty() ? -1 : g->r[0].rank, g->ntiles, g->tilesX, g->tw,
+                        g->th, g->useRccl ? 1 : 0, g->frame};
+  for (int i = 0; i < n && i < 9; ++i) info[i] = v[i];
+  return RT_OK;
+}
+
+int rt_group_plan(const rt_group* g, int32_t* owner, int32_t* order, int cap) {
+  if (!g) return set_error(RT_E_INVALID, "rt_group_plan: null group");
+  for (int i = 0; i < g->ntiles && i < cap; ++i) {
+    if (owner) owner[i] = g->owner[i];
+    if (order) order[i] = g->order[i];
+  }
+  return g->ntiles;
+}
+
+int rt_group_rank_pixels(const rt_group* g, int rank, int32_t* pixels, int64_t cap) {
+  if (!g || rank < 0 || rank >= g->world) return set_error(RT_E_INVALID, "rt_group_rank_pixels: bad arguments");
+  std::vector<int32_t> a, b, c, d;
+  rank_lists(g, rank, a, b, c, d);
+  for (int64_t i = 0; i < (int64_t)d.size() && i < cap && pixels; ++i) pixels[i] = d[i];
+  return (int)std::min<int64_t>(d.size(), INT32_MAX);
+}
+
+int rt_group_kernel_ms(rt_group* g, int rank, double* avg_ms, int* frames) {
+  if (!g || !avg_ms) return set_error(RT_E_INVALID, "rt_group_kernel_ms: null argument");
+  GRank* R = local_rank(g, rank);
+  if (!R) return set_error(RT_E_INVALID, "rt_group_kernel_ms: rank not driven by this process");
+  GCHK(hipSetDevice(R->dev));
+  GCHK(hipStreamSynchronize(R->st));
+  const int64_t m = std::min<int64_t>(R->timed, KRING);
+  double sum = 0;
+  for (int64_t k = 0; k < m; ++k) {
+    const int64_t f = R->timed - 1 - k;
+    float ms = 0;
+    GCHK(hipEventElapsedTime(&ms, R->tA[f % KRING], R->tB[f % KRING]));
+    sum += ms;
+  }
+  *avg_ms = m ? sum / m : 0.0;
+  if (frames) *frames = (int)m;
+  R->timed = 0;
+  return RT_OK;
+}
+
+// One rank's step alone (the one-process emulation on one GPU): its render, pack,
+// copy into rank 0's slab and the scatter of its slice -- rank 0: its render and the scatter of the
+// whole slab -- frames pipelined as rt_group_render pipelines them; wall-clock time per step and the
+// mean HIP-event time of its render.
+int rt_group_time_rank(rt_group* g, int rank, int warmup, int iters, double* step_ms, double* kernel_ms) {
+  if (!g || iters <= 0 || !step_ms || !kernel_ms) return set_error(RT_E_INVALID, "rt_group_time_rank: bad arguments");
+  if (g->rankMode || g->useRccl) return set_error(RT_E_INVALID, "rt_group_time_rank: one-process RT_GROUP_COPY groups only");
+  GRank* R = local_rank(g, rank);
+  GRank* R0 = local_rank(g, 0);
+  if (!R || !R0) return set_error(RT_E_INVALID, "rt_group_time_rank: bad rank");
+  int rc;
+  auto step = [&](int64_t f) -> int {
+    const int b = (int)(f & 1);
+    if (rank == 0) {
+      if ((rc = enqueue_render(g, *R, g->outRgb, g->outArgb, true))) return rc;
+      GCHK(hipSetDevice(R0->dev));
+      GCHK(hipStreamWaitEvent(R0->cs, g->evRecv[b], 0));
+      if ((rc = enqueue_scatter(g, R0->cs, b, 0, g->nRecv, g->outRgb, g->outArgb))) return rc;
+      GCHK(hipEventRecord(g->evRecv[b], R0->cs));
+      return RT_OK;
+    }
+    if ((rc = enqueue_render(g, *R, R->fRgb, R->fArgb, true)) || (rc = enqueue_pack(g, *R, b))) return rc;
+    const size_t n = R->hAll.size();
+    GCHK(hipStreamWaitEvent(R->cs, g->evRecv[b], 0));
+    if (n) {
+      GCHK(hipMemcpyPeerAsync(g->rArgb[b] + R->off, g->rootDev, R->sArgb[b], R->dev, n * sizeof(int32_t), R->cs));
+      if (g->rgb) GCHK(hipMemcpyPeerAsync(g->rRgb[b] + 3 * R->off, g->rootDev, R->sRgb[b], R->dev, n * 12, R->cs));
+    }
+    GCHK(hipEventRecord(R->evSent[b], R->cs));
+    if (R->dev == R0->dev) {
+      if ((rc = enqueue_scatter(g, R->cs, b, R->off, R->off + (int64_t)n, g->outRgb, g->outArgb))) return rc;
+      GCHK(hipEventRecord(g->evRecv[b], R->cs));
+    }
+    return RT_OK;
+  };
+  for (int i = 0; i < warmup; ++i)
+    if ((rc = step(i))) return rc;
+  if ((rc = sync_group(g))) return rc;
+  R->timed = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < iters; ++i)
+    if ((rc = step(warmup + i))) return rc;
+  if ((rc = sync_group(g))) return rc;
+  const auto t1 = std::chrono::steady_clock::now();
+  *step_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() / iters;
+  int fr = 0;
+  return rt_group_kernel_ms(g, rank, kernel_ms, &fr);
+}
+
+int rt_group_count(rt_group* g, int rank, uint64_t* stats) {
+  if (!g || !stats) return set_error(RT_E_INVALID, "rt_group_count: null argument");
+  GRank* R = local_rank(g, rank);
+  if (!R) return set_error(RT_E_INVALID, "rt_group_count: rank not driven by this process");
+  std::vector<int32_t> t = R->hTiles;
+  t.insert(t.end(), R->hSplit.begin(), R->hSplit.end());
+  for (int i = 0; i < RT_ST_N; ++i) stats[i] = 0;
+  if (t.empty()) return RT_OK;
+  return rt_render_tiles_count(R->s, &g->p, t.data(), (int)t.size(), stats);
+}
+
+void rt_group_destroy(rt_group* g) { (void)destroy_group(g); }
+
+}  // extern "C"

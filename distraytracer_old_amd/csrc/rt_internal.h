@@ -11,6 +11,15 @@ namespace rt {
 
 int set_error(int code, const std::string& msg);
 
+// Quarter-octave bucket of a measured wave time (dispatch order key, longest first): 0 for 0, else
+// 1 + floor(4 log2 c) by exact threshold compares (trace.hip sort_tiles, group.hip plan_ranks).
+inline int cost_bucket(uint32_t c) {
+  if (!c) return 0;
+  const int oct = 31 - __builtin_clz(c);
+  const double f = (double)c / (double)(1u << oct);  // [1, 2)
+  return 1 + 4 * oct + (f >= 1.6817928305074290) + (f >= 1.4142135623730951) + (f >= 1.1892071150027210);
+}
+
 // Flattened scene on the host (mirrors SceneD) -- built by scene_build.cpp.
 struct HostScene {
   std::vector<XformD> xf;
@@ -64,6 +73,18 @@ namespace rt {
 // photon_build.hip: the same structure built on the scene's device (n > PHOTON_LEAF)
 // (with the reference's kd-tree after the BVH records, built on the device too)
 int build_photon_tree_gpu(rt_scene* s, const double* pos, const double* pwr, int64_t n);
+// trace.hip: the render launches the multi-GPU group (group.hip) drives. prepare_render fills the
+// kernel parameters of a render (rt_render_params checks, wave layout, camera constants);
+// launch_tile_list renders a validated DEVICE tile list, launch_pixel_list a validated DEVICE pixel
+// list one sample per wave (per-sample colours in smpCol[npix * spp * 3] / smpTr[npix * spp]);
+// both asynchronous on `stream` (hipStream_t).
+int prepare_render(rt_scene* s, const rt_render_params* p, ParamsD& P);
+int launch_tile_list(rt_scene* s, const ParamsD& P, uint32_t flags, const int32_t* dtiles, int ntiles, float* rgb,
+                     int32_t* argb, void* stream);
+int launch_pixel_list(rt_scene* s, const ParamsD& P, uint32_t flags, const int32_t* dpix, int npix, double* smpCol,
+                      uint8_t* smpTr, float* rgb, int32_t* argb, void* stream);
+// group.hip: the deterministic rank plan (rt_rank_plan)
+void plan_ranks(const uint32_t* cost, int n, int world, double heavy, int slots, int32_t* owner, int32_t* order);
 }  // namespace rt
 
 struct rt_scene {
@@ -96,9 +117,10 @@ struct rt_scene {
     void* measured = nullptr;  // hipEvent_t recorded after the measuring launch, on its stream
   };
   std::vector<TileSchedule> schedules;
-  struct TileList {  // rt_render_tiles_device: a validated tile list and its device copy
+  struct TileList {  // rt_render_tiles_device / rt_render_pixels_device: a validated list and its device copy
     std::vector<int32_t> host;
     int32_t* dev = nullptr;
+    int32_t maxv = -1;  // its largest entry: a reuse checks it against the new layout's bound
   };
   std::vector<TileList> tileLists;
   // RT_RENDER_WAVEFRONT buffers (grow-only): level-0 records, sample colours, traced flags, level

@@ -432,7 +432,12 @@ static int make_params(rt_scene* s, const rt_render_params* p, ParamsD& P) {
   // RT_RENDER_PIXEL_WAVES: one pixel per wave (64 sample lanes, those past spp idle) -- the same
   // samples in the same order per pixel, so the same image; the multi-GPU split renders its
   // heaviest tiles this way (their 2 x 2 pixels in four waves at once)
-  if (p->flags & RT_RENDER_PIXEL_WAVES) G = 64;
+  if (p->flags & RT_RENDER_PIXEL_WAVES) {
+    // (at spp = 1 the kernel's one-sample path keeps the colour as traced; the 64-lane layout would
+    // sum it from 0, turning -0.0 into +0.0)
+    if (P.spp < 2) return set_error(RT_E_INVALID, "RT_RENDER_PIXEL_WAVES needs spp >= 2");
+    G = 64;
+  }
   static const int TW[7] = {8, 8, 4, 4, 2, 2, 1};  // pixels per wave 64, 32, ..., 1 as tw x th
   int lg = 0;
   while ((1 << lg) < G) ++lg;
@@ -525,6 +530,31 @@ static RenderFn pick_variant(const HostScene& h, uint32_t flags) {
     if ((f & ~v.mask) == 0) return v.fn;
   return dv::render_kernel<false, dv::FT_ALL>;
 }
+// the feature mask of the variant pick_variant launches (without RT_RENDER_SHCOMPACT)
+static uint32_t variant_mask(const HostScene& h, uint32_t flags) {
+  const uint32_t f = (flags & RT_RENDER_GENERIC) ? (uint32_t)dv::FT_ALL : scene_features(h);
+  for (const Variant& v : kVariants)
+    if ((f & ~v.mask) == 0) return v.mask;
+  return dv::FT_ALL;
+}
+
+// Instrumented (counting) instantiations of the timed variants the benchmark configs run -- C3's
+// (triangles only: nearest-first BVH traversal compiled in), C4's and C5's -- so the counted record
+// loads are the ones the timed kernel issues (bench.py's roofline numerator); other scenes count
+// with the all-features kernel.
+static const Variant kCountVariants[] = {
+    {0u, dv::render_kernel<true, 0u>},
+    {dv::FT_PRIM | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX,
+     dv::render_kernel<true, dv::FT_PRIM | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX>},
+    {dv::F_C5, dv::render_kernel<true, dv::F_C5>},
+    {dv::FT_ALL, dv::render_kernel<true, dv::FT_ALL>},
+};
+static const Variant& count_variant(const HostScene& h, uint32_t flags) {
+  const uint32_t m = (flags & RT_RENDER_SHCOMPACT) ? (uint32_t)dv::FT_ALL : variant_mask(h, flags);
+  for (const Variant& v : kCountVariants)
+    if (v.mask == m) return v;
+  return kCountVariants[sizeof(kCountVariants) / sizeof(kCountVariants[0]) - 1];
+}
 
 // Dispatch schedule: tiles sorted by cost, longest first, so the long tiles do not end
 // up in the tail of the launch (matters most for the small per-GPU launches of a
@@ -551,13 +581,7 @@ static int sort_tiles(rt_scene::TileSchedule& e, hipStream_t st) {
   std::vector<uint8_t> key(e.ntiles);
   int hist[NB] = {0};
   for (int i = 0; i < e.ntiles; ++i) {
-    const uint32_t c = cost[i];
-    int k = 0;
-    if (c) {
-      const int oct = 31 - __builtin_clz(c);
-      const double f = (double)c / (double)(1u << oct);  // [1, 2)
-      k = 1 + 4 * oct + (f >= 1.6817928305074290) + (f >= 1.4142135623730951) + (f >= 1.1892071150027210);
-    }
+    const int k = cost_bucket(cost[i]);
     key[i] = (uint8_t)k;
     hist[k]++;
   }
@@ -641,26 +665,35 @@ static int render_wf(rt_scene* s, const SceneD& sd, const ParamsD& P, float* d_r
       (rc = wf_grow(s, R::WF_Q1, 2 * slots * sizeof(WfRay))))
     return rc;
   const int dof = ((F & dv::FT_DOF) && sd.dof && !((F & dv::FT_CAMX) && P.cam != 0)) ? 1 : 0;
+  // queue capacity divisor: a testing knob (DISTRAYTRACER_WF_QCAP_DIV, default 1) that undersizes the
+  // queues so that the device's overflow guard, and its error word, are exercised
+  int qdiv = 1;
+  if (const char* e = std::getenv("DISTRAYTRACER_WF_QCAP_DIV")) qdiv = std::max(1, std::atoi(e));
   for (int t0 = 0; t0 < ntiles; t0 += chunk) {
     const int n = std::min(chunk, ntiles - t0), units = n * rounds;
     int* cnt = (int*)s->wf[R::WF_CNT];
+    int* err = cnt + 15;  // the device's error word: bit 0 a parent out of range, bit 1 a dropped child
     HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(int), st));
     WfNode* node0 = (WfNode*)s->wf[R::WF_NODE0];
     double* scol = (double*)s->wf[R::WF_SCOL];
     uint8_t* straced = (uint8_t*)s->wf[R::WF_TRACED];
     hipLaunchKernelGGL(dv::wf_camera_kernel<F>, dim3(units), dim3(64), dv::LDS_RENDER_BYTES, st, sd, P, t0, rounds, node0,
-                       scol, straced, (WfRay*)s->wf[R::WF_Q1], cnt + 1, (int32_t)(2 * (size_t)units * 64));
+                       scol, straced, (WfRay*)s->wf[R::WF_Q1], cnt + 1, (int32_t)(2 * (size_t)units * 64 / qdiv), err);
     HIPCHK(hipGetLastError());
     int counts[9] = {0};
     int L = 1;
+    int cap = (int)(2 * (size_t)units * 64 / qdiv);  // the capacity the producing launch wrote its queue with
     for (; L <= 7; ++L) {  // level L reads queue L % 2 (WF_Q0 / WF_Q1), writes the other one
-      int c = 0;
+      int c = 0, bad = 0;
       HIPCHK(hipMemcpyAsync(&c, cnt + L, sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&bad, err, sizeof(int), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
+      if (bad || c > cap)  // the device dropped a ray or a delivery: stop before anything reads the queue
+        return set_error(RT_E_HIP, std::string("RT_RENDER_WAVEFRONT: the device dropped ") +
+                                       ((bad & 1) ? "a delivery (parent out of range)" : "a queued ray (queue capacity)"));
       if (c == 0) break;
-      if (c > (L == 1 ? 2 * units * 64 : 2 * counts[L - 1]))
-        return set_error(RT_E_HIP, "RT_RENDER_WAVEFRONT: a ray queue overflowed");
       counts[L] = c;
+      cap = 2 * c / qdiv;
       const int qin = (L % 2) ? R::WF_Q1 : R::WF_Q0, qout = (L % 2) ? R::WF_Q0 : R::WF_Q1;
       if ((rc = wf_grow(s, R::WF_NODE1 + L - 1, (size_t)c * sizeof(WfNode))) ||
           (rc = wf_grow(s, qout, (size_t)2 * c * sizeof(WfRay))))
@@ -669,20 +702,26 @@ static int render_wf(rt_scene* s, const SceneD& sd, const ParamsD& P, float* d_r
       const int32_t nPrev = L == 1 ? units * 64 : counts[L - 1];
       hipLaunchKernelGGL(dv::wf_level_kernel<F>, dim3((unsigned)((c + 63) / 64)), dim3(64), dv::LDS_RENDER_BYTES, st, sd, P,
                          (const WfRay*)s->wf[qin], cnt + L, (WfNode*)s->wf[R::WF_NODE1 + L - 1], prev, nPrev,
-                         (WfRay*)s->wf[qout], cnt + L + 1, 2 * c);
+                         (WfRay*)s->wf[qout], cnt + L + 1, cap, err);
       HIPCHK(hipGetLastError());
     }
     for (int l = L - 1; l >= 1; --l) {  // bottom up: a level's frames into their parents
       WfNode* prev = l == 1 ? node0 : (WfNode*)s->wf[R::WF_NODE1 + l - 2];
       const int32_t nPrev = l == 1 ? units * 64 : counts[l - 1];
       hipLaunchKernelGGL(dv::wf_fold_kernel<F>, dim3((unsigned)((counts[l] + 255) / 256)), dim3(256), 0, st, sd,
-                         (const WfNode*)s->wf[R::WF_NODE1 + l - 1], cnt + l, 0, prev, nPrev, scol);
+                         (const WfNode*)s->wf[R::WF_NODE1 + l - 1], cnt + l, 0, prev, nPrev, scol, err);
     }
     hipLaunchKernelGGL(dv::wf_fold_kernel<F>, dim3((unsigned)((units * 64 + 255) / 256)), dim3(256), 0, st, sd,
-                       (const WfNode*)node0, (const int*)nullptr, units * 64, (WfNode*)nullptr, 0, scol);
+                       (const WfNode*)node0, (const int*)nullptr, units * 64, (WfNode*)nullptr, 0, scol, err);
     hipLaunchKernelGGL(dv::wf_final_kernel<F>, dim3(n), dim3(64), 0, st, P, t0, rounds, (const double*)scol,
                        (const uint8_t*)straced, d_rgb, d_argb, dof);
     HIPCHK(hipGetLastError());
+    int bad = 0;
+    HIPCHK(hipMemcpyAsync(&bad, err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (bad)
+      return set_error(RT_E_HIP, std::string("RT_RENDER_WAVEFRONT: the device dropped a ") +
+                                     ((bad & 2) ? "queued ray (queue capacity)" : "delivery (parent out of range)"));
   }
   return RT_OK;
 }
@@ -695,6 +734,15 @@ static int render_wavefront(rt_scene* s, const SceneD& sd, const ParamsD& P, uin
   return render_wf<dv::FT_ALL>(s, sd, P, d_rgb, d_argb, st);
 }
 
+// the scene view a launch uses: nearest-first / wave-cull bits, or the reference's full scan
+static SceneD launch_scene(const rt_scene* s, uint32_t flags) {
+  SceneD sd = s->dev;
+  sd.fastSlab |= SCENE_NEAREST_FIRST;
+  if (sd.ntop <= 64 && !(flags & RT_RENDER_NOWAVECULL)) sd.fastSlab |= SCENE_WAVE_CULL;
+  if (flags & RT_RENDER_NOCULL) { sd.topBound = s->noCullBound; sd.fastSlab &= ~(SCENE_NEAREST_FIRST | SCENE_WAVE_CULL); }
+  return sd;
+}
+
 // tiles: an explicit tile list (rt_render_tiles_device) -- ntiles blocks, block b renders tiles[b]
 static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, int32_t* d_argb, bool count,
                   hipStream_t st, const int32_t* tiles = nullptr, int ntiles = 0) {
@@ -703,10 +751,7 @@ static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, 
   dim3 grid(dv::xcd_grid(tilesX * tilesY)), block(64);
   if ((flags & RT_RENDER_WAVEFRONT) && !count) {
     if (tiles) return set_error(RT_E_INVALID, "RT_RENDER_WAVEFRONT renders whole layouts, not tile lists");
-    SceneD sd = s->dev;
-    sd.fastSlab |= SCENE_NEAREST_FIRST;
-    if (sd.ntop <= 64 && !(flags & RT_RENDER_NOWAVECULL)) sd.fastSlab |= SCENE_WAVE_CULL;
-    if (flags & RT_RENDER_NOCULL) { sd.topBound = s->noCullBound; sd.fastSlab &= ~(SCENE_NEAREST_FIRST | SCENE_WAVE_CULL); }
+    const SceneD sd = launch_scene(s, flags);
     if (P.colStep != 1) return set_error(RT_E_INVALID, "RT_RENDER_WAVEFRONT: not for refine passes");
     return render_wavefront(s, sd, P, flags, d_rgb, d_argb, st);
   }
@@ -721,13 +766,10 @@ static int launch(rt_scene* s, const ParamsD& P0, uint32_t flags, float* d_rgb, 
     if (rc) return rc;
   }
 #endif
-  SceneD sd = s->dev;
-  sd.fastSlab |= SCENE_NEAREST_FIRST;
-  if (sd.ntop <= 64 && !(flags & RT_RENDER_NOWAVECULL)) sd.fastSlab |= SCENE_WAVE_CULL;
-  if (flags & RT_RENDER_NOCULL) { sd.topBound = s->noCullBound; sd.fastSlab &= ~(SCENE_NEAREST_FIRST | SCENE_WAVE_CULL); }
-  if (count) {  // counting always runs the all-features kernel
+  const SceneD sd = launch_scene(s, flags);
+  if (count) {  // the counting instantiation of the timed variant (count_variant)
     HIPCHK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long) * RT_ST_N, st));
-    hipLaunchKernelGGL((dv::render_kernel<true, dv::FT_ALL>), grid, block, dv::LDS_RENDER_BYTES, st, sd, P, d_rgb, d_argb,
+    hipLaunchKernelGGL(count_variant(s->hs, flags).fn, grid, block, dv::LDS_RENDER_BYTES, st, sd, P, d_rgb, d_argb,
                        (unsigned long long*)s->counters);
   } else {
     hipLaunchKernelGGL(pick_variant(s->hs, flags), grid, block, dv::LDS_RENDER_BYTES, st, sd, P, d_rgb, d_argb,
@@ -854,6 +896,13 @@ int rt_photon_gather(rt_scene* s, const double* pts, double* out, int64_t n) {
   return RT_OK;
 }
 
+int rt_render_variant(const rt_scene* s, uint32_t flags, uint32_t* timed, uint32_t* counted) {
+  if (!s) return set_error(RT_E_INVALID, "rt_render_variant: null scene");
+  if (timed) *timed = variant_mask(s->hs, flags);
+  if (counted) *counted = count_variant(s->hs, flags).mask;
+  return RT_OK;
+}
+
 int rt_render_count(rt_scene* s, const rt_render_params* p, float* rgb, int32_t* argb, uint64_t* stats) {
   if (!stats) return set_error(RT_E_INVALID, "null stats");
   return render_host(s, p, rgb, argb, stats);
@@ -931,9 +980,14 @@ static int tile_list(rt_scene* s, const ParamsD& P, const int32_t* tiles, int nt
   rt_scene::TileList* L = nullptr;
   for (auto& x : s->tileLists)
     if (x.host.size() == (size_t)ntiles && std::memcmp(x.host.data(), tiles, sizeof(int32_t) * ntiles) == 0) { L = &x; break; }
+  // a cached list (maybe validated as a pixel list, against another bound) is reused only below this layout's
+  if (L && L->maxv >= lay[0]) return set_error(RT_E_INVALID, "tile list: tile index out of range");
   if (!L) {
-    for (int i = 0; i < ntiles; ++i)
+    int32_t mx = -1;
+    for (int i = 0; i < ntiles; ++i) {
       if (tiles[i] < 0 || tiles[i] >= lay[0]) return set_error(RT_E_INVALID, "tile list: tile index out of range");
+      mx = std::max(mx, tiles[i]);
+    }
     if (s->tileLists.size() >= 16) {  // oldest out (its launches may be on streams we do not know: drain the device)
       HIPCHK(hipDeviceSynchronize());
       (void)hipFree(s->tileLists.front().dev);
@@ -941,6 +995,7 @@ static int tile_list(rt_scene* s, const ParamsD& P, const int32_t* tiles, int nt
     }
     rt_scene::TileList t;
     t.host.assign(tiles, tiles + ntiles);
+    t.maxv = mx;
     HIPCHK(hipMalloc(&t.dev, sizeof(int32_t) * ntiles));
     HIPCHK(hipMemcpy(t.dev, tiles, sizeof(int32_t) * ntiles, hipMemcpyHostToDevice));
     s->tileLists.push_back(std::move(t));
@@ -983,15 +1038,28 @@ int rt_render_tiles_count(rt_scene* s, const rt_render_params* p, const int32_t*
 }  // extern "C"
 
 template <uint32_t F>
-static int launch_pixels(rt_scene* s, const SceneD& sd, const ParamsD& P, const int32_t* dpix, int npix, float* d_rgb,
-                         int32_t* d_argb, hipStream_t st) {
+static int launch_pixels(const SceneD& sd, const ParamsD& P, const int32_t* dpix, int npix, double* smpCol,
+                         uint8_t* smpTr, float* d_rgb, int32_t* d_argb, hipStream_t st) {
   const int dof = ((F & dv::FT_DOF) && sd.dof && !((F & dv::FT_CAMX) && P.cam != 0)) ? 1 : 0;
   hipLaunchKernelGGL(dv::sample_kernel<F>, dim3((unsigned)((int64_t)npix * P.spp)), dim3(64), dv::LDS_RENDER_BYTES, st, sd,
-                     P, dpix, (double*)s->smpCol, (uint8_t*)s->smpTr);
+                     P, dpix, smpCol, smpTr);
   hipLaunchKernelGGL(dv::pixel_sum_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, P, dpix, npix,
-                     (const double*)s->smpCol, (const uint8_t*)s->smpTr, d_rgb, d_argb, dof);
+                     (const double*)smpCol, (const uint8_t*)smpTr, d_rgb, d_argb, dof);
   HIPCHK(hipGetLastError());
   return RT_OK;
+}
+
+// one sample per wave for a device pixel list (validated by the caller), per-sample colours in
+// smpCol[npix * spp * 3] / smpTr[npix * spp]
+static int pixel_samples(rt_scene* s, const ParamsD& P, uint32_t flags, const int32_t* dpix, int npix, double* smpCol,
+                         uint8_t* smpTr, float* d_rgb, int32_t* d_argb, hipStream_t st) {
+  const SceneD sd = launch_scene(s, flags);
+  const uint32_t f = (flags & RT_RENDER_GENERIC) ? (uint32_t)dv::FT_ALL : scene_features(s->hs);
+  constexpr uint32_t C4 = dv::FT_PRIM | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX;
+  if (f == 0) return launch_pixels<0u>(sd, P, dpix, npix, smpCol, smpTr, d_rgb, d_argb, st);
+  if ((f & ~dv::F_C5) == 0) return launch_pixels<dv::F_C5>(sd, P, dpix, npix, smpCol, smpTr, d_rgb, d_argb, st);
+  if ((f & ~C4) == 0) return launch_pixels<C4>(sd, P, dpix, npix, smpCol, smpTr, d_rgb, d_argb, st);
+  return launch_pixels<dv::FT_ALL>(sd, P, dpix, npix, smpCol, smpTr, d_rgb, d_argb, st);
 }
 
 extern "C" {
@@ -1023,6 +1091,7 @@ int rt_render_pixels_device(rt_scene* s, const rt_render_params* p, const int32_
       }
       rt_scene::TileList t;
       t.host.assign(pixels, pixels + npix);
+      t.maxv = *std::max_element(pixels, pixels + npix);
       HIPCHK(hipMalloc(&t.dev, sizeof(int32_t) * npix));
       HIPCHK(hipMemcpy(t.dev, pixels, sizeof(int32_t) * npix, hipMemcpyHostToDevice));
       s->tileLists.push_back(std::move(t));
@@ -1041,17 +1110,8 @@ int rt_render_pixels_device(rt_scene* s, const rt_render_params* p, const int32_
     HIPCHK(hipMalloc(&s->smpTr, ns));
     s->smpCap = ns;
   }
-  SceneD sd = s->dev;
-  sd.fastSlab |= SCENE_NEAREST_FIRST;
-  if (sd.ntop <= 64 && !(p->flags & RT_RENDER_NOWAVECULL)) sd.fastSlab |= SCENE_WAVE_CULL;
-  if (p->flags & RT_RENDER_NOCULL) { sd.topBound = s->noCullBound; sd.fastSlab &= ~(SCENE_NEAREST_FIRST | SCENE_WAVE_CULL); }
-  hipStream_t st = (hipStream_t)stream;
-  const uint32_t f = (p->flags & RT_RENDER_GENERIC) ? (uint32_t)dv::FT_ALL : scene_features(s->hs);
-  constexpr uint32_t C4 = dv::FT_PRIM | dv::FT_TRANS | dv::FT_TEX | dv::FT_LIGHTX;
-  if (f == 0) return launch_pixels<0u>(s, sd, P, dpix, npix, d_rgb, d_argb, st);
-  if ((f & ~dv::F_C5) == 0) return launch_pixels<dv::F_C5>(s, sd, P, dpix, npix, d_rgb, d_argb, st);
-  if ((f & ~C4) == 0) return launch_pixels<C4>(s, sd, P, dpix, npix, d_rgb, d_argb, st);
-  return launch_pixels<dv::FT_ALL>(s, sd, P, dpix, npix, d_rgb, d_argb, st);
+  return pixel_samples(s, P, p->flags, dpix, npix, (double*)s->smpCol, (uint8_t*)s->smpTr, d_rgb, d_argb,
+                       (hipStream_t)stream);
 }
 
 int rt_render_tiles_device(rt_scene* s, const rt_render_params* p, const int32_t* tiles, int ntiles, float* d_rgb,
@@ -1335,4 +1395,20 @@ extern "C" int rt_scene_photon_map(const rt_scene* s, void* nodes, int64_t node_
   if (ppos && np > 0) HIPCHK(hipMemcpy(ppos, s->dev.ppos, sizeof(double) * 3 * np, hipMemcpyDeviceToHost));
   if (ppwr && np > 0) HIPCHK(hipMemcpy(ppwr, s->dev.ppwr, sizeof(double) * 3 * np, hipMemcpyDeviceToHost));
   return RT_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// internal entry points of the multi-GPU group (group.hip, rt_internal.h)
+int rt::prepare_render(rt_scene* s, const rt_render_params* p, ParamsD& P) { return make_params(s, p, P); }
+
+int rt::launch_tile_list(rt_scene* s, const ParamsD& P, uint32_t flags, const int32_t* dtiles, int ntiles, float* rgb,
+                         int32_t* argb, void* stream) {
+  if (ntiles <= 0) return RT_OK;
+  return launch(s, P, flags & ~(uint32_t)RT_RENDER_WAVEFRONT, rgb, argb, false, (hipStream_t)stream, dtiles, ntiles);
+}
+
+int rt::launch_pixel_list(rt_scene* s, const ParamsD& P, uint32_t flags, const int32_t* dpix, int npix, double* smpCol,
+                          uint8_t* smpTr, float* rgb, int32_t* argb, void* stream) {
+  if (npix <= 0) return RT_OK;
+  return pixel_samples(s, P, flags, dpix, npix, smpCol, smpTr, rgb, argb, (hipStream_t)stream);
 }

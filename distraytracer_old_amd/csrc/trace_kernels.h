@@ -1939,7 +1939,8 @@ DEVI void knn_hist_pass(const SceneD& S, const double* pos, double lo, double hi
 // getIrradianceFromPhtnTree (myObjShader.java:441-458): the powers summed in poll order (farthest
 // first) over pi * (the first polled d2). The heap and the recursion's frames live in the wave's pkT
 // LDS levels (idle once the counting selection's final pass is done); the lane runs alone.
-static_assert(KNN_MAX * 12 + 64 * 4 <= PK_LDS * 64 * 8, "the replay's heap and frames fit the pkT levels");
+// PriorityQueue.offer adds before poll trims: the heap holds K + 1 entries for a moment (K <= KNN_MAX)
+static_assert((KNN_MAX + 1) * 12 + 64 * 4 <= PK_LDS * 64 * 8, "the replay's heap and frames fit the pkT levels");
 #ifndef RT_KNN_JAVA_CALL  // the replay as a real call: the hot variants' register allocation stays as it was
 #define RT_KNN_JAVA_CALL 1
 #endif
@@ -1954,9 +1955,9 @@ KNN_JAVA_FN V knn_java_(const NodeD* pnode, const double* ppos, const double* pp
   const int32_t off = pnode[root].padR[2];
   if (off <= 0) return mk(0, 0, 0);  // no kd-tree (unreachable: every photon map carries one)
   const KdNodeD* kd = reinterpret_cast<const KdNodeD*>(pnode + off);
-  lds_f64* hd = pkT();                               // queue: d2
-  lds_i32* hx = (lds_i32*)(pkT() + KNN_MAX);         // queue: photon (leaf order)
-  lds_i32* stk = hx + KNN_MAX;                       // frames: node << 2 | stage
+  lds_f64* hd = pkT();                               // queue: d2 (K + 1 slots: offer, then poll)
+  lds_i32* hx = (lds_i32*)(pkT() + KNN_MAX + 1);     // queue: photon (leaf order)
+  lds_i32* stk = hx + KNN_MAX + 1;                   // frames: node << 2 | stage
   int n = 0;
   auto poll = [&]() {  // PriorityQueue.poll: the root goes, the last element sifts down from it
     --n;

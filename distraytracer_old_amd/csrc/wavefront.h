@@ -189,14 +189,20 @@ DEVI V wf_fold(const SceneD& S, const WfNode& P) {
   return clampc(add(local, acc));
 }
 DEVI void wf_put(double* dst, V c) { dst[0] = c.x; dst[1] = c.y; dst[2] = c.z; }
-DEVI void wf_deliver(WfNode* prev, int32_t nPrev, int32_t parent, V c) {
-  if ((uint32_t)(parent >> 1) >= (uint32_t)nPrev) return;  // (a parent outside the previous level: never)
+// A parent outside the previous level or a child past the queue's capacity would be an indexing bug:
+// it is not written, and the launch's error word is set (render_wf returns RT_E_HIP for it).
+DEVI void wf_deliver(WfNode* prev, int32_t nPrev, int32_t parent, V c, int* __restrict__ err) {
+  if ((uint32_t)(parent >> 1) >= (uint32_t)nPrev) {
+    atomicOr(err, 1);
+    return;
+  }
   WfNode& p = prev[parent >> 1];
   wf_put((parent & 1) ? p.cB : p.cA, c);
 }
 
 // children of a wave into the next level's queue: ballot + mbcnt prefix counts, one atomic add
-DEVI void wf_emit(const WfOut& r, int32_t me, const Key& k, WfRay* __restrict__ qout, int* __restrict__ cntOut, int32_t qcap) {
+DEVI void wf_emit(const WfOut& r, int32_t me, const Key& k, WfRay* __restrict__ qout, int* __restrict__ cntOut, int32_t qcap,
+                  int* __restrict__ err) {
   const uint64_t b1 = __ballot(r.nch >= 1), b2 = __ballot(r.nch == 2);
   if (!(b1 | b2)) return;
   const uint32_t tot = (uint32_t)(__popcll(b1) + __popcll(b2));
@@ -207,7 +213,10 @@ DEVI void wf_emit(const WfOut& r, int32_t me, const Key& k, WfRay* __restrict__ 
   const uint32_t below = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u));
   const uint32_t below2 = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b2, 0u));
   auto put = [&](int slot, const Child& c, int side) {
-    if (slot >= qcap) return;  // (at most two children per ray: the queue holds them all)
+    if (slot >= qcap) {  // (at most two children per ray: the queue holds them all)
+      atomicOr(err, 2);
+      return;
+    }
     WfRay& q = qout[slot];
     q.o[0] = c.o.x; q.o[1] = c.o.y; q.o[2] = c.o.z;
     q.d[0] = c.d.x; q.d[1] = c.d.y; q.d[2] = c.d.z;
@@ -222,7 +231,8 @@ DEVI void wf_emit(const WfOut& r, int32_t me, const Key& k, WfRay* __restrict__ 
 template <uint32_t F>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WF_WAVES)))
 wf_camera_kernel(SceneD S, ParamsD P, int tile0, int rounds, WfNode* __restrict__ node0, double* __restrict__ scol,
-                 uint8_t* __restrict__ straced, WfRay* __restrict__ qout, int* __restrict__ cntOut, int32_t qcap) {
+                 uint8_t* __restrict__ straced, WfRay* __restrict__ qout, int* __restrict__ cntOut, int32_t qcap,
+                 int* __restrict__ err) {
   const int lane = threadIdx.x;
   const int unit = blockIdx.x, tile = tile0 + unit / rounds, round = unit % rounds;
   const int me = unit * 64 + lane;
@@ -265,7 +275,7 @@ wf_camera_kernel(SceneD S, ParamsD P, int tile0, int rounds, WfNode* __restrict_
   }
   straced[me] = traced ? 1 : 0;
   if (r.nch == 0) wf_put(scol + 3 * (size_t)me, r.c);
-  wf_emit(r, me, k, qout, cntOut, qcap);
+  wf_emit(r, me, k, qout, cntOut, qcap, err);
 }
 
 // level L >= 1: every queued ray of the level
@@ -273,7 +283,7 @@ template <uint32_t F>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WF_WAVES)))
 wf_level_kernel(SceneD S, ParamsD P, const WfRay* __restrict__ qin, const int* __restrict__ cntIn,
                 WfNode* __restrict__ nodeL, WfNode* __restrict__ nodePrev, int32_t nPrev, WfRay* __restrict__ qout,
-                int* __restrict__ cntOut, int32_t qcap) {
+                int* __restrict__ cntOut, int32_t qcap, int* __restrict__ err) {
   const int me = blockIdx.x * 64 + threadIdx.x;
   if (blockIdx.x * 64 >= *cntIn) return;  // whole wave past the queue
   const bool live = me < *cntIn;
@@ -293,24 +303,24 @@ wf_level_kernel(SceneD S, ParamsD P, const WfRay* __restrict__ qin, const int* _
     k.pixel = q.pixel; k.sample = q.sample;
     parent = q.parent;
     r = wf_shade<F>(S, in, k, nodeL[me]);
-    if (r.nch == 0) wf_deliver(nodePrev, nPrev, parent, r.c);
+    if (r.nch == 0) wf_deliver(nodePrev, nPrev, parent, r.c, err);
     else nodeL[me].parent = parent;  // where this frame's fold delivers
   }
-  wf_emit(r, me, k, qout, cntOut, qcap);
+  wf_emit(r, me, k, qout, cntOut, qcap, err);
 }
 
 // fold of one level's frames into their parents (level 0: into the sample colours)
 template <uint32_t F>
 __global__ void __launch_bounds__(256) wf_fold_kernel(SceneD S, const WfNode* __restrict__ nodeL, const int* __restrict__ cnt,
                                                       int n0, WfNode* __restrict__ nodePrev, int32_t nPrev,
-                                                      double* __restrict__ scol) {
+                                                      double* __restrict__ scol, int* __restrict__ err) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int n = cnt ? *cnt : n0;
   if (i >= n) return;
   const WfNode& P = nodeL[i];
   if (!P.kind) return;
   const V c = wf_fold<F>(S, P);
-  if (nodePrev) wf_deliver(nodePrev, nPrev, P.parent, c);
+  if (nodePrev) wf_deliver(nodePrev, nPrev, P.parent, c, err);
   else wf_put(scol + 3 * (size_t)i, c);
 }
 

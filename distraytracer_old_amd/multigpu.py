@@ -41,11 +41,18 @@ def max_tile_rows(world: int, H: int, band: int = BAND) -> int:
 
 
 def cost_bucket(costs):
-    """Quarter-octave cost buckets (the single-GPU schedule's sort key, trace.hip sort_tiles): -1 for 0."""
+    """Quarter-octave cost buckets (the dispatch sort key, rt_internal.h cost_bucket): 0 for 0, else
+    1 + floor(4 log2 c) by exact compares of c / 2^floor(log2 c) against 2^(1/4), 2^(1/2), 2^(3/4)."""
     import numpy as np
 
     c = np.asarray(costs, dtype=np.float64)
-    return np.where(c > 0, np.floor(4.0 * np.log2(np.maximum(c, 1.0))), -1.0)
+    oct_ = np.floor(np.log2(np.maximum(c, 1.0)))
+    # the octave from the float log2 can be off by one at exact powers of two: fix it exactly
+    oct_ = np.where(np.exp2(oct_) > c, oct_ - 1, oct_)
+    oct_ = np.where(np.exp2(oct_ + 1) <= c, oct_ + 1, oct_)
+    f = c / np.exp2(oct_)
+    k = 1 + 4 * oct_ + (f >= 1.6817928305074290) + (f >= 1.4142135623730951) + (f >= 1.1892071150027210)
+    return np.where(c > 0, k, 0.0)
 
 
 def contiguous_tiles(costs, world: int) -> list:
@@ -124,11 +131,12 @@ class RankPlan:
     per wave (rt_render_pixels_device, mode "sample") or one pixel per wave (RT_RENDER_PIXEL_WAVES,
     mode "pixel": a 2 x 2-pixel tile's four pixels in four waves)."""
 
-    def __init__(self, tiles, pixels, mode="sample"):
+    def __init__(self, tiles, pixels, mode="sample", split=()):
         import numpy as np
 
         self.tiles = np.ascontiguousarray(tiles, dtype=np.int32)
         self.pixels = np.ascontiguousarray(pixels, dtype=np.int32)
+        self.split = np.ascontiguousarray(split, dtype=np.int32)  # the tiles whose pixels `pixels` are
         self.mode = mode
 
     def pixel_list(self, tiles_x: int, tw: int, th: int, W: int, H: int):
@@ -157,7 +165,7 @@ def rank_plans(costs, world: int, tiles_x: int, tw: int, th: int, W: int, H: int
     out = []
     for t in parts:
         hv = c[t] > thr
-        out.append(RankPlan(t[~hv], tile_pixels(t[hv], tiles_x, tw, th, W, H), mode))
+        out.append(RankPlan(t[~hv], tile_pixels(t[hv], tiles_x, tw, th, W, H), mode, t[hv]))
     return out
 
 

@@ -49,7 +49,11 @@ EXPORTS = ["rt_abi_version", "rt_build_id", "rt_last_error", "rt_device_count", 
            "rt_png_name", "rt_scene_save_name", "rt_math_eval", "rt_tile_layout", "rt_tile_costs",
            "rt_render_tiles_device", "rt_render_tiles_count",
            "rt_render_pixels_device", "rt_photon_gather",
-           "rt_photon_kdtree", "rt_scene_photon_kdtree"]
+           "rt_photon_kdtree", "rt_scene_photon_kdtree",
+           # ABI 6: the multi-GPU frame (rt_group_*), the kernel variants
+           "rt_render_variant", "rt_rank_plan", "rt_group_unique_id", "rt_group_create", "rt_group_create_rank", "rt_group_render",
+           "rt_group_sync", "rt_group_render_host", "rt_group_frame", "rt_group_info", "rt_group_plan",
+           "rt_group_rank_pixels", "rt_group_kernel_ms", "rt_group_time_rank", "rt_group_count", "rt_group_destroy"]
 
 _lib = None
 
@@ -120,6 +124,28 @@ def lib():
         L.rt_math_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
         L.rt_png_name.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
         L.rt_scene_save_name.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
+        if hasattr(L, "rt_group_create"):  # ABI >= 6
+            vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
+            L.rt_rank_plan.argtypes = [vp, i32, i32, dbl, i32, vp, vp]
+            L.rt_render_variant.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                            ctypes.POINTER(ctypes.c_uint32)]
+            L.rt_group_unique_id.argtypes = [vp, i32]
+            L.rt_group_create.argtypes = [vp, i32, ctypes.POINTER(RenderParams), ctypes.c_uint32, dbl, i32,
+                                          ctypes.POINTER(vp)]
+            L.rt_group_create_rank.argtypes = [vp, i32, i32, vp, ctypes.POINTER(RenderParams), ctypes.c_uint32, dbl,
+                                               i32, ctypes.POINTER(vp)]
+            L.rt_group_render.argtypes = [vp, vp, vp]
+            L.rt_group_sync.argtypes = [vp]
+            L.rt_group_render_host.argtypes = [vp, vp, vp]
+            L.rt_group_frame.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+            L.rt_group_info.argtypes = [vp, vp, i32]
+            L.rt_group_plan.argtypes = [vp, vp, vp, i32]
+            L.rt_group_rank_pixels.argtypes = [vp, i32, vp, i64]
+            L.rt_group_kernel_ms.argtypes = [vp, i32, ctypes.POINTER(dbl), ctypes.POINTER(i32)]
+            L.rt_group_time_rank.argtypes = [vp, i32, i32, i32, ctypes.POINTER(dbl), ctypes.POINTER(dbl)]
+            L.rt_group_count.argtypes = [vp, i32, vp]
+            L.rt_group_destroy.argtypes = [vp]
+            L.rt_group_destroy.restype = None
         _lib = L
     return _lib
 
@@ -163,6 +189,146 @@ def photon_kdtree(pos) -> np.ndarray:
     out = np.zeros((len(pos), 4), dtype=np.int32)
     _check(lib().rt_photon_kdtree(pos.ctypes.data, len(pos), out.ctypes.data), "rt_photon_kdtree")
     return out
+
+
+def rank_plan(cost, world: int, heavy: float = 0.0, slots: int = 0):
+    """The deterministic multi-GPU plan of a layout's tile costs (rt_rank_plan, host only):
+    (owner int32 [ntiles], order int32 [ntiles]) -- owner[t] in [0, world) renders tile t in its wave
+    run, world + r marks one of rank r's split (one sample per wave) tiles; order = dispatch order."""
+    c = np.ascontiguousarray(cost, dtype=np.uint32)
+    owner = np.zeros(len(c), dtype=np.int32)
+    order = np.zeros(len(c), dtype=np.int32)
+    _check(lib().rt_rank_plan(c.ctypes.data, len(c), world, heavy, slots, owner.ctypes.data, order.ctypes.data),
+           "rt_rank_plan")
+    return owner, order
+
+
+def group_unique_id() -> bytes:
+    """128-byte RCCL unique id for rt_group_create_rank (call on rank 0, share with the others)."""
+    buf = ctypes.create_string_buffer(128)
+    n = lib().rt_group_unique_id(buf, 128)
+    if n < 0:
+        raise RTError(f"rt_group_unique_id failed ({n}): {lib().rt_last_error().decode()}")
+    return buf.raw[:n]
+
+
+GROUP_RGB = 1  # RT_GROUP_RGB: exchange the float-RGB plane too
+GROUP_COPY = 2  # RT_GROUP_COPY: device copies in one process (ranks may share a device)
+GROUP_INFO = ["world", "local_ranks", "first_rank", "ntiles", "tiles_x", "tw", "th", "rccl", "frames"]
+
+
+class Group:
+    """A multi-GPU frame (rt_group_*): one process driving N ranks (`create`) or one rank per
+    process (`create_rank`). render() enqueues a frame; rank 0's frame lands in its own device
+    buffers (frame()) or in caller-owned ones."""
+
+    def __init__(self, handle, scenes):
+        self._h = handle
+        self._scenes = scenes  # keep the scenes alive while the group uses them
+
+    @classmethod
+    def create(cls, scenes, W, H, spp=0, seed=0x5EED0001, flags=0, rgb=False, copy=False, heavy=0.0, slots=0):
+        p = params(W, H, spp, seed, None, 1, flags, 1)
+        arr = (ctypes.c_void_p * len(scenes))(*[s._h for s in scenes])
+        h = ctypes.c_void_p()
+        gf = (GROUP_RGB if rgb else 0) | (GROUP_COPY if copy else 0)
+        _check(lib().rt_group_create(arr, len(scenes), ctypes.byref(p), gf, heavy, slots, ctypes.byref(h)),
+               "rt_group_create")
+        return cls(h, list(scenes))
+
+    @classmethod
+    def create_rank(cls, scene, rank, world, uid, W, H, spp=0, seed=0x5EED0001, flags=0, rgb=False, heavy=0.0,
+                    slots=0):
+        p = params(W, H, spp, seed, None, 1, flags, 1)
+        h = ctypes.c_void_p()
+        u = ctypes.create_string_buffer(bytes(uid), 128) if uid is not None else None
+        _check(lib().rt_group_create_rank(scene._h, rank, world, u, ctypes.byref(p), GROUP_RGB if rgb else 0, heavy,
+                                          slots, ctypes.byref(h)), "rt_group_create_rank")
+        return cls(h, [scene])
+
+    def render(self, rgb_ptr: int = 0, argb_ptr: int = 0):
+        _check(lib().rt_group_render(self._h, ctypes.c_void_p(rgb_ptr or None), ctypes.c_void_p(argb_ptr or None)),
+               "rt_group_render")
+
+    def sync(self):
+        _check(lib().rt_group_sync(self._h), "rt_group_sync")
+
+    def render_host(self, W, H, rgb=True):
+        """Blocking frame into host arrays (rank 0's process): (rgb [H, W, 3] float32 or None, argb [H, W])."""
+        a = np.zeros((H, W), dtype=np.int32)
+        c = np.zeros((H, W, 3), dtype=np.float32) if rgb else None
+        _check(lib().rt_group_render_host(self._h, c.ctypes.data if rgb else None, a.ctypes.data),
+               "rt_group_render_host")
+        return c, a
+
+    def frame(self):
+        """Device pointers (rgb or 0, argb) of the group's own frame on rank 0's device."""
+        r, a = ctypes.c_void_p(), ctypes.c_void_p()
+        _check(lib().rt_group_frame(self._h, ctypes.byref(r), ctypes.byref(a)), "rt_group_frame")
+        return r.value or 0, a.value or 0
+
+    def info(self) -> dict:
+        v = np.zeros(len(GROUP_INFO), dtype=np.int64)
+        _check(lib().rt_group_info(self._h, v.ctypes.data, len(v)), "rt_group_info")
+        return dict(zip(GROUP_INFO, v.tolist()))
+
+    def plan(self):
+        n = self.info()["ntiles"]
+        owner = np.zeros(n, dtype=np.int32)
+        order = np.zeros(n, dtype=np.int32)
+        r = lib().rt_group_plan(self._h, owner.ctypes.data, order.ctypes.data, n)
+        if r < 0:
+            raise RTError(f"rt_group_plan: {lib().rt_last_error().decode()}")
+        return owner, order
+
+    def rank_tiles(self, rank: int):
+        """(run tiles, split tiles) of a rank in dispatch order."""
+        owner, order = self.plan()
+        world = self.info()["world"]
+        o = owner[order]
+        return order[o == rank], order[o == world + rank]
+
+    def rank_pixels(self, rank: int) -> np.ndarray:
+        n = lib().rt_group_rank_pixels(self._h, rank, None, 0)
+        if n < 0:
+            raise RTError(f"rt_group_rank_pixels: {lib().rt_last_error().decode()}")
+        out = np.zeros(n, dtype=np.int32)
+        lib().rt_group_rank_pixels(self._h, rank, out.ctypes.data, n)
+        return out
+
+    def kernel_ms(self, rank: int):
+        ms, fr = ctypes.c_double(0), ctypes.c_int(0)
+        _check(lib().rt_group_kernel_ms(self._h, rank, ctypes.byref(ms), ctypes.byref(fr)), "rt_group_kernel_ms")
+        return ms.value, fr.value
+
+    def time_rank(self, rank: int, warmup: int = 3, iters: int = 20):
+        """(wall ms per step, mean render ms) of one rank's pipelined step alone (RT_GROUP_COPY groups)."""
+        a, b = ctypes.c_double(0), ctypes.c_double(0)
+        _check(lib().rt_group_time_rank(self._h, rank, warmup, iters, ctypes.byref(a), ctypes.byref(b)),
+               "rt_group_time_rank")
+        return a.value, b.value
+
+    def count(self, rank: int) -> dict:
+        st = np.zeros(RT_ST_N, dtype=np.uint64)
+        _check(lib().rt_group_count(self._h, rank, st.ctypes.data), "rt_group_count")
+        return dict(zip(ST_NAMES, st[: len(ST_NAMES)].tolist()))
+
+    def close(self):
+        if self._h:
+            lib().rt_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 def device_count() -> int:
@@ -315,6 +481,12 @@ class Scene:
         _check(lib().rt_render_count(self._h, ctypes.byref(p), rgb.ctypes.data, argb.ctypes.data, st.ctypes.data),
                "rt_render_count")
         return rgb, argb, dict(zip(ST_NAMES, st[: len(ST_NAMES)].tolist()))
+
+    def variant(self, flags: int = 0) -> tuple[int, int]:
+        """(timed, counted) feature masks F of the render_kernel<CNT, F> instantiations (rt_render_variant)."""
+        a, b = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        _check(lib().rt_render_variant(self._h, flags, ctypes.byref(a), ctypes.byref(b)), "rt_render_variant")
+        return a.value, b.value
 
     def render_device(self, p: RenderParams, rgb_ptr: int, argb_ptr: int, stream: int = 0):
         """Asynchronous render into device buffers (e.g. torch tensors' data_ptr()) on a HIP stream."""

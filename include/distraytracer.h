@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 enum rt_status {
   RT_OK = 0,
@@ -305,9 +305,76 @@ int rt_render_pass(rt_scene* scene, const rt_render_params* p, int step, int ski
    slower; stats: uint64[RT_ST_N] (24 since ABI 4). RT_RENDER_NOCULL in p->flags counts the
    reference algorithm's work (every objList entry tested). */
 int rt_render_count(rt_scene* scene, const rt_render_params* p, float* rgb, int32_t* argb, uint64_t* stats);
+/* The render-kernel instantiations a scene's renders use (ABI 6), as feature masks (the template
+   argument F of render_kernel<CNT, F>, csrc/trace_kernels.h FT_*): *timed = the variant rt_render
+   launches with `flags`, *counted = the counting variant rt_render_count launches -- the same mask for
+   the benchmark configs' variants (C3 0, C4, C5), so the counted record loads are the timed kernel's. */
+int rt_render_variant(const rt_scene* scene, uint32_t flags, uint32_t* timed, uint32_t* counted);
 /* Kernel-only timing helper: average ms of the render kernel over `iters` launches (HIP events on the
    launch stream), inputs resident in HBM; at least 2 warmup launches (the schedule calibration). */
 int rt_time_render(rt_scene* scene, const rt_render_params* p, int warmup, int iters, double* avg_ms);
+
+/* ---- Multi-GPU frame (ABI 6) ---------------------------------------
+   The reference's draw() (myScene.java:1481-1531) over N GPUs: the whole-frame layout's wave tiles,
+   measured once on rank 0 (rt_tile_costs), are cut into N contiguous runs of equal cost, and the
+   tiles whose own wave would outlast a rank's share are rendered one sample per wave beside them
+   (rt_rank_plan). Every frame each rank renders its part into a device frame, ranks > 0 pack their
+   pixels and send them to rank 0 (RCCL point-to-point over xGMI, grouped), and rank 0 -- which
+   rendered its own part straight into the output frame -- scatters them in. Frame f's exchange
+   overlaps frame f + 1's render (double-buffered slabs on a third stream per rank). The frame is
+   bit-identical to rt_render's for every N and transport. */
+typedef struct rt_group rt_group;
+/* rt_group_create flags */
+#define RT_GROUP_RGB 1u  /* exchange the float-RGB plane too (default: the ARGB ints, rndrdImg.pixels) */
+#define RT_GROUP_COPY 2u /* transport: device / peer copies in this process instead of RCCL; ranks may
+                            share a device (the one-GPU emulation of an N-GPU frame) */
+/* The deterministic plan of a layout's tile costs (host only): owner[t] = the rank rendering tile t
+   in its wave run, or world + rank when the tile is one of that rank's split (one sample per wave)
+   tiles; order[0..ntiles) = every tile in dispatch order (longest first by quarter-octave cost
+   bucket, row-major inside a bucket): a rank's run and split tiles are the subsequences of order it
+   owns. heavy <= 0: 1.25 (a tile is split when its cost exceeds heavy x total / (slots x world));
+   slots <= 0: 4096 (wave slots of one MI355X at the render kernel's occupancy). */
+int rt_rank_plan(const uint32_t* cost, int ntiles, int world, double heavy, int slots, int32_t* owner, int32_t* order);
+/* One process, n ranks: scenes[i] (rt_scene_create / rt_scene_load_cli on its device) is rank i.
+   RCCL transport (ncclCommInitAll; one distinct device per rank) unless RT_GROUP_COPY. p: the frame
+   (width, height, spp, seed, flags; row fields ignored). Calibrates the layout on scenes[0]. */
+int rt_group_create(rt_scene* const* scenes, int n, const rt_render_params* p, uint32_t flags, double heavy, int slots,
+                    rt_group** out);
+/* One process per GPU: this process is `rank` of `world` (collective: every rank calls it). unique_id:
+   the 128 bytes rt_group_unique_id returned on rank 0, shared by the caller (e.g. over
+   torch.distributed); rank 0 calibrates and broadcasts the tile costs over RCCL. */
+int rt_group_unique_id(void* id, int cap);
+int rt_group_create_rank(rt_scene* scene, int rank, int world, const void* unique_id, const rt_render_params* p,
+                         uint32_t flags, double heavy, int slots, rt_group** out);
+/* Enqueue one frame (asynchronous). d_rgb / d_argb: rank 0's output frame, device buffers on its
+   device (rgb float[H*W*3] needs RT_GROUP_RGB; NULL: the group's own frame, rt_group_frame); ignored
+   in processes without rank 0. rt_group_sync waits for every stream of the ranks this process drives. */
+int rt_group_render(rt_group* g, float* d_rgb, int32_t* d_argb);
+int rt_group_sync(rt_group* g);
+/* Blocking frame into caller-owned HOST buffers (either may be NULL) on rank 0's process -- the JNI
+   draw() over N GPUs; other processes render their part and return. */
+int rt_group_render_host(rt_group* g, float* rgb, int32_t* argb);
+int rt_group_frame(rt_group* g, float** d_rgb, int32_t** d_argb);
+/* info[0..8]: world, ranks driven by this process, first of them, layout tiles, tiles_x, tw, th,
+   transport (1 RCCL / 0 copies), frames enqueued */
+int rt_group_info(const rt_group* g, int64_t* info, int n);
+/* the plan (rt_rank_plan's owner / order, up to cap tiles); returns the tile count */
+int rt_group_plan(const rt_group* g, int32_t* owner, int32_t* order, int cap);
+/* every pixel (row * width + col) rank `rank` writes, in the order it sends them (its run's tiles,
+   then its split pixels); returns the count */
+int rt_group_rank_pixels(const rt_group* g, int rank, int32_t* pixels, int64_t cap);
+/* mean HIP-event time of a driven rank's render (run + split pixels) over its frames since the last
+   call (up to the last 64); synchronises that rank's render stream */
+int rt_group_kernel_ms(rt_group* g, int rank, double* avg_ms, int* frames);
+/* One-process RT_GROUP_COPY groups: `rank`'s step alone, frames pipelined as rt_group_render does
+   (render, pack, copy into rank 0's slab, the scatter of its slice; rank 0: render + the whole
+   scatter): wall-clock ms per step and the mean HIP-event ms of its render (the N-GPU step's
+   non-kernel cost, measured on one GPU) */
+int rt_group_time_rank(rt_group* g, int rank, int warmup, int iters, double* step_ms, double* kernel_ms);
+/* counters (rt_render_count's) of a driven rank's part: its run and its split tiles (counted as tile
+   waves; blocking) */
+int rt_group_count(rt_group* g, int rank, uint64_t* stats);
+void rt_group_destroy(rt_group* g);
 
 /* Diagnostics: the device's fdlibm sin / cos / asin / acos (the sequences the trace kernels use,
    shared bit for bit with the CPU oracle) of x[0..n) into out[4*i .. 4*i+3], host buffers. */

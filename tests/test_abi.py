@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(rt.EXPORTS)
-    assert L.rt_abi_version() == 5
+    assert L.rt_abi_version() == 6
     # provenance: the library carries the build id of the sources and flags it was built from
     from distraytracer_old_amd import build
     assert rt.build_id() == build.built_id() == build.build_id()
@@ -121,3 +121,10 @@ def test_every_reference_scene_loads():
 # (loadImage returns null there and the skydome lookup fails at render time)
 MISSING_IN_REFERENCE = {"planets3backup.cli": "sky_offworld2a.jpg"}
 IGNORED_COMMAND_SCENES = ["c2torus.cli", "old_t07a.cli", "rect_test.cli", "p4_t06Alt.cli", "c4InSphere.cli"]
+
+
+def test_group_unique_id_loads_rccl():
+    """The multi-GPU group's RCCL transport is resolved at run time (dlopen): the library finds RCCL
+    and hands out a 128-byte unique id without a GPU (ncclGetUniqueId needs none)."""
+    u = rt.group_unique_id()
+    assert len(u) == 128 and any(u)

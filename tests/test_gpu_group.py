@@ -1,0 +1,134 @@
+"""The multi-GPU frame behind the C ABI (rt_group_*, csrc/group.hip; VERDICT r04 Next #1).
+
+* N = 1 through the group equals rt_render bit for bit (float RGB and ARGB);
+* the one-process emulation (RT_GROUP_COPY, every rank on device 0) of N = 2 / 3 / 8 ranks
+  reassembles the 1-GPU frame bit for bit -- the plans' wave runs, their split pixels (one sample
+  per wave on the side stream), the pack, the device-copy exchange into rank 0's slab and the
+  scatter -- on C3's scene, the photon-map scene (t11) and C4's transparent / textured scene;
+* frames are pipelined (double-buffered slabs): several frames in flight deliver the same image;
+* the native plan equals the Python restatement on the measured costs, and the group's per-rank
+  pixel lists partition the frame;
+* rank mode (one process per GPU) at world 1 is the same frame.
+"""
+import numpy as np
+import pytest
+
+from distraytracer_old_amd import multigpu, rt, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(cli, seed=None):
+    g = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+    if g.info()["photon_mode"]:
+        g.build_photons(seed)
+    return g
+
+
+CASES = [("c3_bun69k.cli", 320, 256, 4, 0x5EED0001),     # >= 2^16 pixels: measured (scheduled) costs
+         ("t11.cli", 256, 256, 4, 0x5EED0005),            # photon map
+         ("plnts3ColsBunnies.cli", 256, 256, 2, 0x5EED0004)]  # C4's variant: glass, textures, spot lights
+
+
+@pytest.mark.parametrize("case", CASES, ids=["c3", "t11", "c4"])
+def test_group_one_rank_equals_rt_render(case):
+    cli, W, H, spp, seed = case
+    g = _scene(cli, seed)
+    rgb, argb = g.render(W, H, spp=spp, seed=seed)
+    with rt.Group.create([g], W, H, spp=spp, seed=seed, rgb=True) as grp:
+        assert grp.info()["world"] == 1 and grp.info()["rccl"] == 0
+        for _ in range(2):
+            c, a = grp.render_host(W, H)
+            assert np.array_equal(a, argb)
+            assert np.array_equal(c.view(np.uint32), rgb.view(np.uint32))
+    # rank mode at world 1: no communicator, the same frame
+    with rt.Group.create_rank(g, 0, 1, None, W, H, spp=spp, seed=seed) as grp:
+        _, a = grp.render_host(W, H, rgb=False)
+        assert np.array_equal(a, argb)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("case", CASES, ids=["c3", "t11", "c4"])
+def test_group_emulated_ranks_reassemble_the_frame(case, world):
+    cli, W, H, spp, seed = case
+    g = _scene(cli, seed)
+    rgb, argb = g.render(W, H, spp=spp, seed=seed)
+    # heavy = 0.1, slots = 64: tiles above ~1-4x the mean wave time are split, so the split path runs
+    with rt.Group.create([g] * world, W, H, spp=spp, seed=seed, rgb=True, copy=True, heavy=0.1, slots=64) as grp:
+        owner, order = grp.plan()
+        assert (owner >= world).any(), "no tile was split: the one-sample-per-wave path is not exercised"
+        pix = np.concatenate([grp.rank_pixels(r) for r in range(world)])
+        assert np.array_equal(np.sort(pix), np.arange(W * H))
+        c, a = grp.render_host(W, H)
+        assert np.array_equal(a, argb)
+        assert np.array_equal(c.view(np.uint32), rgb.view(np.uint32))
+
+
+def test_group_pipelined_frames_and_device_outputs():
+    """Frames in flight (no sync between them) into caller-owned device frames: every one complete."""
+    import torch
+
+    cli, W, H, spp, seed = CASES[0]
+    g = _scene(cli)
+    rgb, argb = g.render(W, H, spp=spp, seed=seed)
+    world = 4
+    with rt.Group.create([g] * world, W, H, spp=spp, seed=seed, rgb=True, copy=True, heavy=0.1, slots=64) as grp:
+        outs = [(torch.full((H, W, 3), -1.0, device="cuda"), torch.zeros((H, W), dtype=torch.int32, device="cuda"))
+                for _ in range(5)]
+        torch.cuda.synchronize()
+        for o in outs:
+            grp.render(o[0].data_ptr(), o[1].data_ptr())
+        grp.sync()
+        for c, a in outs:
+            assert np.array_equal(a.cpu().numpy(), argb)
+            assert np.array_equal(c.cpu().numpy().view(np.uint32), rgb.view(np.uint32))
+        ms, frames = grp.kernel_ms(0)
+        assert frames == 5 and ms > 0
+
+
+def test_group_plan_equals_python_on_measured_costs():
+    cli, W, H, spp, seed = CASES[0]
+    g = _scene(cli)
+    p = rt.params(W, H, spp=spp, seed=seed)
+    n, tx, tw, th = g.tile_layout(p)
+    with rt.Group.create([g] * 8, W, H, spp=spp, seed=seed, copy=True) as grp:
+        cost = g.tile_costs(p)  # the layout's wave times, measured once (by the group's calibration)
+        owner, order = grp.plan()
+        o2, d2 = rt.rank_plan(cost, 8)
+        assert np.array_equal(owner, o2) and np.array_equal(order, d2)
+        py = multigpu.rank_plans(cost, 8, tx, tw, th, W, H)
+        for r in range(8):
+            run, split = grp.rank_tiles(r)
+            assert np.array_equal(run, py[r].tiles)
+            assert np.array_equal(multigpu.tile_pixels(split, tx, tw, th, W, H), py[r].pixels)
+            assert np.array_equal(grp.rank_pixels(r), py[r].pixel_list(tx, tw, th, W, H))
+
+
+def test_group_time_rank_reports_step_and_kernel():
+    cli, W, H, spp, seed = CASES[0]
+    g = _scene(cli)
+    with rt.Group.create([g] * 4, W, H, spp=spp, seed=seed, copy=True) as grp:
+        for r in range(4):
+            step, kern = grp.time_rank(r, warmup=2, iters=5)
+            assert step > 0 and kern > 0
+
+
+def test_group_counts_cover_the_frame():
+    """rt_group_count over the ranks sums to the whole frame's camera samples."""
+    cli, W, H, spp, seed = CASES[0]
+    g = _scene(cli)
+    with rt.Group.create([g] * 3, W, H, spp=spp, seed=seed, copy=True, heavy=0.1, slots=64) as grp:
+        cams = sum(grp.count(r)["camera"] for r in range(3))
+    assert cams == W * H * spp
+
+
+def test_group_rejects_bad_arguments():
+    cli, W, H, spp, seed = CASES[0]
+    g = _scene(cli)
+    with pytest.raises(rt.RTError):  # RCCL needs one device per rank
+        rt.Group.create([g, g], W, H, spp=spp, seed=seed)
+    with pytest.raises(rt.RTError):
+        rt.Group.create([g], W, H, spp=spp, seed=seed, flags=rt.RENDER_WAVEFRONT)
+    with rt.Group.create([g], W, H, spp=spp, seed=seed) as grp:  # no RT_GROUP_RGB: no float plane
+        with pytest.raises(rt.RTError):
+            grp.render_host(W, H, rgb=True)

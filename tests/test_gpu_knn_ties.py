@@ -114,3 +114,35 @@ def test_device_kdtree_is_the_references(tmp_path, monkeypatch, n):
     assert np.array_equal(dev[:, 1:], host[:, 1:])
     assert np.array_equal(ppos[dev[:, 0]], pos[host[:, 0]])
     assert np.array_equal(ppwr[dev[:, 0]], pwr[host[:, 0]])
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_gather_ties_at_the_largest_k(tmp_path, seed):
+    """k = KNN_MAX = 256, the largest neighbourhood the device takes: PriorityQueue.offer adds before
+    poll trims, so the replay's heap holds 257 entries for a moment (its LDS arrays have
+    K + 1 slots). A 9 x 9 x 5 lattice with duplicated points puts ties across the 256th distance."""
+    k = 256
+    cli = tmp_path / "knn.cli"
+    cli.write_text(f"fov 60\nbackground 0 0 0\npoint_light 0 5 0 1 1 1\ndiffuse_photons 100 {k} 100\n"
+                   "diffuse .5 .5 .5 0 0 0\nsphere 1 0 0 -5\n")
+    rng = np.random.default_rng(seed)
+    grid = np.stack(np.meshgrid(np.arange(-4, 5), np.arange(-4, 5), np.arange(-2, 3), indexing="ij"), -1).reshape(-1, 3)
+    pos = np.concatenate([grid, grid[rng.choice(len(grid), 150, replace=False)]]).astype(np.float64)
+    pos = pos[rng.permutation(len(pos))]
+    pwr = rng.random((len(pos), 3))
+    g = rt.Scene.load_cli("knn.cli", scene_dir=tmp_path, textures={})
+    g.set_photons(pos, pwr)
+    o = OracleScene(tmp_path, "knn.cli")
+    o.set_photons(pos, pwr)
+    qs = np.concatenate([np.array([(0.0, 0.0, 0.0), (0.5, 0.0, 0.0), (0.5, 0.5, 0.5), (1.0, -1.0, 0.0)]),
+                         rng.integers(-4, 5, size=(28, 3)) * 0.5, rng.uniform(-2, 2, size=(32, 3))])
+    got = g.photon_gather(qs)
+    ties = 0
+    for q, gv in zip(qs, got):
+        ev, straddle = _oracle_irradiance(o, pos, pwr, q, k)
+        if straddle:
+            ties += 1
+            assert np.array_equal(gv, ev), (q, gv, ev)
+        else:
+            np.testing.assert_allclose(gv, ev, rtol=1e-12, atol=0)
+    assert ties >= 5

@@ -130,8 +130,10 @@ def test_ray_counts_match_oracle(cli, W, spp):
     so = dict(so, implicit=so["sphere"])
     for k in ("camera", "shadow", "refl", "refr", "tri", "quad", "implicit", "light", "texel"):
         assert sg[k] == so[k], (k, sg[k], so[k])
-    # per-wave record loads never exceed the per-lane ones; culling only removes work (the counting
-    # kernel is the all-features variant: reference child order in every BVH)
+    # per-wave record loads never exceed the per-lane ones; culling and the nearest-first order only
+    # remove work (the counting kernel is the timed variant's instantiation, rt_render_variant)
+    timed, counted = g.variant()
+    assert timed == counted
     _, _, sc = g.render_count(W, W, spp=spp, seed=SEED)
     for k in ("node", "tri", "quad", "implicit", "light", "photon"):
         assert sc["w_" + k] <= sc[k], k
@@ -380,6 +382,35 @@ def test_wavefront_renders_identically(cli, W, spp):
         rb, ab = g.render(W, W, spp=spp, seed=SEED, flags=flags)
         assert np.array_equal(aa, ab), flags
         assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32)), flags
+
+
+def test_wavefront_undersized_queue_is_an_error(monkeypatch):
+    """The level-synchronous path's device guards are loud: with the queue
+    capacity deliberately undersized (DISTRAYTRACER_WF_QCAP_DIV) the device drops children past it,
+    sets its error word and the render returns RT_E_HIP instead of a wrong image; at the true
+    capacity the same scene renders the plain image."""
+    g = rt.Scene.load_cli("plnts3ColsBunnies.cli", textures=scenes.prepare("plnts3ColsBunnies.cli"))
+    ra, aa = g.render(96, 96, spp=2, seed=SEED)
+    monkeypatch.setenv("DISTRAYTRACER_WF_QCAP_DIV", "8")
+    with pytest.raises(rt.RTError, match="dropped"):
+        g.render(96, 96, spp=2, seed=SEED, flags=rt.RENDER_WAVEFRONT)
+    monkeypatch.setenv("DISTRAYTRACER_WF_QCAP_DIV", "1")
+    rb, ab = g.render(96, 96, spp=2, seed=SEED, flags=rt.RENDER_WAVEFRONT)
+    assert np.array_equal(aa, ab) and np.array_equal(ra.view(np.uint32), rb.view(np.uint32))
+
+
+def test_pixel_waves_render_identically():
+    """RT_RENDER_PIXEL_WAVES (one pixel per wave, 64 sample lanes, those past spp idle; the multi-GPU
+    split's per-pixel mode) renders the plain image -- spp a power of two and not -- and is refused at
+    spp = 1, where the 64-lane layout would sum a pixel's single colour from 0."""
+    g = rt.Scene.load_cli("plnts3ColsBunnies.cli", textures=scenes.prepare("plnts3ColsBunnies.cli"))
+    for spp in (2, 6):
+        ra, aa = g.render(64, 64, spp=spp, seed=SEED)
+        rb, ab = g.render(64, 64, spp=spp, seed=SEED, flags=rt.RENDER_PIXEL_WAVES)
+        assert np.array_equal(aa, ab), spp
+        assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32)), spp
+    with pytest.raises(rt.RTError, match="spp >= 2"):
+        g.render(64, 64, spp=1, seed=SEED, flags=rt.RENDER_PIXEL_WAVES)
 
 
 def test_wavefront_c4_oracle_parity():
