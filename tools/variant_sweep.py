@@ -100,6 +100,7 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "flate": [],                               # shade_node's local colour stored into the frame only when it pushes
     "reslds": [],                              # a finished sample's colour waits in LDS, not in spilled VGPRs
     "reslds0": ["RT_RES_LDS=0"],
+    "inner0": ["RT_KNN_INNER=0"],             # the kNN final pass scans every photon below the window (round 4)
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
