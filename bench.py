@@ -293,6 +293,9 @@ def main():
                                        seed=seed)
         else:
             grp = rt.Group.create([scene], W, H, spp=spp, seed=seed)
+        rank_ms_rebalanced = None
+        if world > 1:  # setup: two re-cuts of the plan from the ranks' measured render times (collective)
+            rank_ms_rebalanced = grp.rebalance(rounds=2, iters=5).tolist()
         run_t, split_t = grp.rank_tiles(rank)
         my_tiles = np.concatenate([run_t, split_t]).astype(np.int32)
         parallelism = ("1 GPU" if world == 1 else
@@ -430,6 +433,7 @@ def main():
                        "parallelism": parallelism},
             "camera_msamples_per_s": cam_frame / (ms_per_step / 1e3) / 1e6,
             "kernel_ms_max_over_ranks": kern_ms_max,
+            "rank_render_ms_after_rebalance": rank_ms_rebalanced if native else None,
             "host_path_ms_per_step": host_ms,
             "host_path": "rt_render into a host ARGB buffer (the JNI draw(), INTEGRATION.md): kernel + "
                          f"{W * H * 4} B read-back to pageable memory, blocking; 1-GPU runs only",

@@ -60,6 +60,7 @@ struct Rccl {
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
   decltype(&ncclBroadcast) bcast = nullptr;
+  decltype(&ncclAllGather) allGather = nullptr;
   decltype(&ncclGetErrorString) errStr = nullptr;
 };
 Rccl g_rccl;
@@ -89,6 +90,7 @@ int rccl_load() {
       sym(R.send, "ncclSend");
       sym(R.recv, "ncclRecv");
       sym(R.bcast, "ncclBroadcast");
+      sym(R.allGather, "ncclAllGather");
       sym(R.errStr, "ncclGetErrorString");
       R.ok = all;
       if (!all) R.why = "librccl.so.1 lacks an entry point the group needs";
@@ -112,19 +114,26 @@ namespace rt {
 // one of that rank's split (one sample per wave) tiles. order: every tile in dispatch order --
 // longest first by quarter-octave cost bucket, row-major inside a bucket; a rank's run and split
 // tiles are the subsequences of `order` it owns.
-void plan_ranks(const uint32_t* cost, int n, int world, double heavy, int slots, int32_t* owner, int32_t* order) {
+void plan_ranks(const uint32_t* cost, int n, int world, double heavy, int slots, int32_t* owner, int32_t* order,
+                const double* weight) {
   // contiguous cut: tile t goes to the rank holding its cost midpoint (prefix sums of integer costs,
-  // exact in double for < 2^53)
+  // exact in double for < 2^53). weight (rt_group_rebalance, may be null): the cut runs over
+  // cost x weight instead -- the ranks' measured speed folded into their tiles' costs
   double total = 0;
   for (int t = 0; t < n; ++t) total += (double)cost[t];
+  double wtotal = total;
+  if (weight) {
+    wtotal = 0;
+    for (int t = 0; t < n; ++t) wtotal += (double)cost[t] * weight[t];
+  }
   double cum = 0;
   for (int t = 0; t < n; ++t) {
-    const double c = (double)cost[t];
+    const double c = weight ? (double)cost[t] * weight[t] : (double)cost[t];
     cum += c;
     int r;
-    if (total > 0) {
+    if (wtotal > 0) {
       const double mid = cum - 0.5 * c;
-      const double q = (mid * world) / total;
+      const double q = (mid * world) / wtotal;
       r = (int)std::min<int64_t>((int64_t)q, world - 1);
     } else {
       r = (int)((int64_t)t * world / std::max(1, n));
@@ -132,6 +141,8 @@ void plan_ranks(const uint32_t* cost, int n, int world, double heavy, int slots,
     owner[t] = r;
   }
   // heavy tiles: a wave longer than `heavy` x a rank's ideal per-slot share is split per sample
+  // (from the measured wave times themselves: whether a wave outlasts a share does not depend on
+  // the rank it lands on)
   if (world > 1) {
     const double thr = heavy * total / ((double)slots * world);
     for (int t = 0; t < n; ++t)
@@ -215,6 +226,10 @@ struct rt_group {
   rt_render_params p{};
   int W = 0, H = 0, ntiles = 0, tilesX = 0, tw = 0, th = 0;
   std::vector<int32_t> owner, order;
+  std::vector<uint32_t> cost;  // the layout's measured wave times (the plan's input)
+  std::vector<double> weight;  // per-tile cut weights (rt_group_rebalance; empty: none)
+  double heavy = 1.25;
+  int slots = 4096;
   std::vector<int64_t> npix;   // pixels written per rank
   std::vector<GRank> r;        // the ranks this process drives (all of them in local mode)
   // rank 0 (root) state
@@ -273,27 +288,13 @@ void rank_lists(const rt_group* g, int q, std::vector<int32_t>& tiles, std::vect
 
 int destroy_group(rt_group* g);
 
-// everything after the plan: per-rank buffers, streams, events, lists; root slabs
-int setup_ranks(rt_group* g) {
-  g->npix.assign(g->world, 0);
-  {
-    std::vector<int32_t> a, b, c, d;
-    for (int q = 0; q < g->world; ++q) {
-      rank_lists(g, q, a, b, c, d);
-      g->npix[q] = (int64_t)d.size();
-    }
-  }
-  int64_t off = 0;
-  std::vector<int64_t> offs(g->world, 0);
-  for (int q = 1; q < g->world; ++q) { offs[q] = off; off += g->npix[q]; }
-  g->nRecv = off;
+// once per group: the per-rank streams and events, rank 0's slab events, the whole-frame buffers
+int setup_streams(rt_group* g) {
   const size_t npx = (size_t)g->W * g->H;
   for (GRank& R : g->r) {
     GCHK(hipSetDevice(R.dev));
     int rc;
     if ((rc = prepare_render(R.s, &g->p, R.P))) return rc;
-    rank_lists(g, R.rank, R.hTiles, R.hSplit, R.hPix, R.hAll);
-    R.off = offs[R.rank];
     GCHK(hipStreamCreateWithFlags(&R.st, hipStreamNonBlocking));
     GCHK(hipStreamCreateWithFlags(&R.side, hipStreamNonBlocking));
     GCHK(hipStreamCreateWithFlags(&R.cs, hipStreamNonBlocking));
@@ -306,18 +307,54 @@ int setup_ranks(rt_group* g) {
       GCHK(hipEventCreate(&R.tA[k]));
       GCHK(hipEventCreate(&R.tB[k]));
     }
+    if (R.rank != 0) {
+      if ((rc = gmalloc(g, (void**)&R.fArgb, npx * sizeof(int32_t)))) return rc;
+      if (g->rgb && (rc = gmalloc(g, (void**)&R.fRgb, npx * 3 * sizeof(float)))) return rc;
+    }
+  }
+  if (g->root) {
+    GCHK(hipSetDevice(g->rootDev));
+    int rc;
+    for (int b2 = 0; b2 < 2; ++b2) GCHK(hipEventCreateWithFlags(&g->evRecv[b2], hipEventDisableTiming));
+    if ((rc = gmalloc(g, (void**)&g->outArgb, npx * sizeof(int32_t)))) return rc;
+    if (g->rgb && (rc = gmalloc(g, (void**)&g->outRgb, npx * 3 * sizeof(float)))) return rc;
+    if (!g->useRccl) {
+      g->evCopied.assign(g->world, nullptr);
+      for (int q = 0; q < g->world; ++q) GCHK(hipEventCreateWithFlags(&g->evCopied[q], hipEventDisableTiming));
+    }
+  }
+  return RT_OK;
+}
+
+// per plan (again after rt_group_rebalance): the ranks' tile / pixel lists on the device, their
+// sample buffers and send slabs, rank 0's scatter list and receive slabs
+int setup_lists(rt_group* g) {
+  g->npix.assign(g->world, 0);
+  {
+    std::vector<int32_t> a, b, c, d;
+    for (int q = 0; q < g->world; ++q) {
+      rank_lists(g, q, a, b, c, d);
+      g->npix[q] = (int64_t)d.size();
+    }
+  }
+  int64_t off = 0;
+  std::vector<int64_t> offs(g->world, 0);
+  for (int q = 1; q < g->world; ++q) { offs[q] = off; off += g->npix[q]; }
+  g->nRecv = off;
+  for (GRank& R : g->r) {
+    GCHK(hipSetDevice(R.dev));
+    int rc;
+    rank_lists(g, R.rank, R.hTiles, R.hSplit, R.hPix, R.hAll);
+    R.off = offs[R.rank];
     if ((rc = gupload(g, R.hTiles, &R.dTiles)) || (rc = gupload(g, R.hPix, &R.dPix)) || (rc = gupload(g, R.hAll, &R.dAll)))
       return rc;
     const size_t ns = R.hPix.size() * (size_t)R.P.spp;
     if ((rc = gmalloc(g, (void**)&R.smpCol, ns * 3 * sizeof(double))) || (rc = gmalloc(g, (void**)&R.smpTr, ns))) return rc;
-    if (R.rank != 0) {
-      if ((rc = gmalloc(g, (void**)&R.fArgb, npx * sizeof(int32_t)))) return rc;
-      if (g->rgb && (rc = gmalloc(g, (void**)&R.fRgb, npx * 3 * sizeof(float)))) return rc;
+    if (R.rank != 0)
       for (int b = 0; b < 2; ++b) {
         if ((rc = gmalloc(g, (void**)&R.sArgb[b], R.hAll.size() * sizeof(int32_t)))) return rc;
         if (g->rgb && (rc = gmalloc(g, (void**)&R.sRgb[b], R.hAll.size() * 3 * sizeof(float)))) return rc;
       }
-    }
   }
   if (g->root) {
     GCHK(hipSetDevice(g->rootDev));
@@ -333,16 +370,14 @@ int setup_ranks(rt_group* g) {
     for (int b2 = 0; b2 < 2; ++b2) {
       if ((rc = gmalloc(g, (void**)&g->rArgb[b2], g->nRecv * sizeof(int32_t)))) return rc;
       if (g->rgb && (rc = gmalloc(g, (void**)&g->rRgb[b2], g->nRecv * 3 * sizeof(float)))) return rc;
-      GCHK(hipEventCreateWithFlags(&g->evRecv[b2], hipEventDisableTiming));
-    }
-    if ((rc = gmalloc(g, (void**)&g->outArgb, npx * sizeof(int32_t)))) return rc;
-    if (g->rgb && (rc = gmalloc(g, (void**)&g->outRgb, npx * 3 * sizeof(float)))) return rc;
-    if (!g->useRccl) {
-      g->evCopied.assign(g->world, nullptr);
-      for (int q = 0; q < g->world; ++q) GCHK(hipEventCreateWithFlags(&g->evCopied[q], hipEventDisableTiming));
     }
   }
   return RT_OK;
+}
+
+int setup_ranks(rt_group* g) {
+  int rc = setup_streams(g);
+  return rc ? rc : setup_lists(g);
 }
 
 int make_layout(rt_group* g, rt_scene* s, const rt_render_params* p, uint32_t flags) {
@@ -368,9 +403,13 @@ int make_layout(rt_group* g, rt_scene* s, const rt_render_params* p, uint32_t fl
 int make_plan(rt_group* g, const std::vector<uint32_t>& cost, double heavy, int slots) {
   if (!(heavy > 0)) heavy = 1.25;
   if (slots <= 0) slots = 4096;
+  g->cost = cost;
+  g->heavy = heavy;
+  g->slots = slots;
   g->owner.assign(g->ntiles, 0);
   g->order.assign(g->ntiles, 0);
-  plan_ranks(cost.data(), g->ntiles, g->world, heavy, slots, g->owner.data(), g->order.data());
+  plan_ranks(cost.data(), g->ntiles, g->world, heavy, slots, g->owner.data(), g->order.data(),
+             g->weight.empty() ? nullptr : g->weight.data());
   return RT_OK;
 }
 
@@ -550,12 +589,13 @@ int destroy_group(rt_group* g) {
 
 extern "C" {
 
-int rt_rank_plan(const uint32_t* cost, int ntiles, int world, double heavy, int slots, int32_t* owner, int32_t* order) {
+int rt_rank_plan(const uint32_t* cost, const double* weight, int ntiles, int world, double heavy, int slots,
+                 int32_t* owner, int32_t* order) {
   if (ntiles < 0 || world < 1 || (ntiles > 0 && (!cost || !owner || !order)))
     return set_error(RT_E_INVALID, "rt_rank_plan: bad arguments");
   if (!(heavy > 0)) heavy = 1.25;
   if (slots <= 0) slots = 4096;
-  plan_ranks(cost, ntiles, world, heavy, slots, owner, order);
+  plan_ranks(cost, ntiles, world, heavy, slots, owner, order, weight);
   return RT_OK;
 }
 
@@ -833,6 +873,61 @@ int rt_group_count(rt_group* g, int rank, uint64_t* stats) {
   for (int i = 0; i < RT_ST_N; ++i) stats[i] = 0;
   if (t.empty()) return RT_OK;
   return rt_render_tiles_count(R->s, &g->p, t.data(), (int)t.size(), stats);
+}
+
+// Re-cut the plan from the ranks' measured render times (collective in rank mode). The cost model
+// (a tile's measured wave time in the 1-GPU calibration) predicts a rank's kernel imperfectly -- waves
+// running together share caches and CUs differently in a rank's compact region than in the whole
+// frame -- so each round times every rank's render (iters frames, HIP events; in the one-process
+// emulation one rank at a time, each with the whole GPU), folds the rank's time per unit of
+// predicted cost into its tiles' cut weights, and cuts again. The split tiles and the dispatch order
+// stay those of the measured wave times; only the cut moves. rank_ms[0..world) (may be NULL) gets the
+// render times of the last measurement, taken after the last cut.
+int rt_group_rebalance(rt_group* g, int rounds, int iters, double* rank_ms) {
+  if (!g || rounds < 0 || iters <= 0) return set_error(RT_E_INVALID, "rt_group_rebalance: bad arguments");
+  if (g->weight.empty()) g->weight.assign(g->ntiles, 1.0);
+  std::vector<double> T(g->world, 0.0);
+  int rc;
+  for (int round = 0; round <= rounds; ++round) {
+    if ((rc = sync_group(g))) return rc;
+    for (GRank& R : g->r) {  // each rank alone (one-process groups share devices)
+      R.timed = 0;
+      const bool r0 = R.rank == 0;
+      for (int i = 0; i < iters; ++i)
+        if ((rc = enqueue_render(g, R, r0 ? g->outRgb : R.fRgb, r0 ? g->outArgb : R.fArgb, true))) return rc;
+      int fr = 0;
+      if ((rc = rt_group_kernel_ms(g, R.rank, &T[R.rank], &fr))) return rc;
+    }
+    if (g->rankMode && g->world > 1) {  // every rank's time to every rank
+      GRank& R = g->r[0];
+      double* d = nullptr;
+      GCHK(hipSetDevice(R.dev));
+      GCHK(hipMalloc(&d, sizeof(double) * (g->world + 1)));
+      hipError_t he = hipMemcpy(d + g->world, &T[R.rank], sizeof(double), hipMemcpyHostToDevice);
+      ncclResult_t nr = ncclSuccess;
+      if (he == hipSuccess) nr = g_rccl.allGather(d + g->world, d, 1, ncclFloat64, R.comm, R.cs);
+      if (he == hipSuccess && nr == ncclSuccess) he = hipStreamSynchronize(R.cs);
+      if (he == hipSuccess && nr == ncclSuccess) he = hipMemcpy(T.data(), d, sizeof(double) * g->world, hipMemcpyDeviceToHost);
+      (void)hipFree(d);
+      if (he != hipSuccess) return set_error(RT_E_HIP, std::string("rebalance all-gather: ") + hipGetErrorString(he));
+      if (nr != ncclSuccess) return set_error(RT_E_HIP, std::string("rebalance all-gather: ") + g_rccl.errStr(nr));
+    }
+    if (round == rounds) break;
+    // a rank's time per unit of weighted cost, relative to the frame's
+    std::vector<double> C(g->world, 0.0);
+    for (int t = 0; t < g->ntiles; ++t) C[g->owner[t] % g->world] += (double)g->cost[t] * g->weight[t];
+    double Tsum = 0, Csum = 0;
+    for (int q = 0; q < g->world; ++q) { Tsum += T[q]; Csum += C[q]; }
+    if (!(Tsum > 0) || !(Csum > 0)) break;
+    std::vector<double> f(g->world, 1.0);
+    for (int q = 0; q < g->world; ++q)
+      if (C[q] > 0 && T[q] > 0) f[q] = (T[q] / Tsum) / (C[q] / Csum);
+    for (int t = 0; t < g->ntiles; ++t) g->weight[t] *= f[g->owner[t] % g->world];
+    if ((rc = make_plan(g, g->cost, g->heavy, g->slots)) || (rc = setup_lists(g))) return rc;
+  }
+  if (rank_ms)
+    for (int q = 0; q < g->world; ++q) rank_ms[q] = T[q];
+  return RT_OK;
 }
 
 void rt_group_destroy(rt_group* g) { (void)destroy_group(g); }

@@ -84,7 +84,8 @@ int launch_tile_list(rt_scene* s, const ParamsD& P, uint32_t flags, const int32_
 int launch_pixel_list(rt_scene* s, const ParamsD& P, uint32_t flags, const int32_t* dpix, int npix, double* smpCol,
                       uint8_t* smpTr, float* rgb, int32_t* argb, void* stream);
 // group.hip: the deterministic rank plan (rt_rank_plan)
-void plan_ranks(const uint32_t* cost, int n, int world, double heavy, int slots, int32_t* owner, int32_t* order);
+void plan_ranks(const uint32_t* cost, int n, int world, double heavy, int slots, int32_t* owner, int32_t* order,
+                const double* weight = nullptr);
 }  // namespace rt
 
 struct rt_scene {

@@ -55,7 +55,7 @@ def cost_bucket(costs):
     return np.where(c > 0, k, 0.0)
 
 
-def contiguous_tiles(costs, world: int) -> list:
+def contiguous_tiles(costs, world: int, weights=None) -> list:
     """Cut the tiles in row-major order into `world` contiguous runs of (nearly) equal measured
     cost (prefix sums; rank r takes the tiles whose cumulative cost midpoint lies in
     [r T / N, (r + 1) T / N)): every rank renders a compact region of the image, so the waves
@@ -64,9 +64,10 @@ def contiguous_tiles(costs, world: int) -> list:
     import numpy as np
 
     c = np.asarray(costs, dtype=np.float64)
-    cum = np.cumsum(c)
+    cw = c if weights is None else c * np.asarray(weights, dtype=np.float64)  # the cut's costs
+    cum = np.cumsum(cw)
     total = cum[-1] if len(cum) else 0.0
-    mid = cum - 0.5 * c
+    mid = cum - 0.5 * cw
     owner = np.minimum((mid * world / max(total, 1e-300)).astype(np.int64), world - 1) if total > 0 else \
         (np.arange(len(c)) * world // max(1, len(c)))
     bucket = cost_bucket(c)
@@ -147,17 +148,18 @@ class RankPlan:
 
 
 def rank_plans(costs, world: int, tiles_x: int, tw: int, th: int, W: int, H: int, mode: str = "cut",
-               heavy: float = HEAVY, slots: int = WAVE_SLOTS, split: str = "sample") -> list:
+               heavy: float = HEAVY, slots: int = WAVE_SLOTS, split: str = "sample", weights=None) -> list:
     """Partition a layout's tiles over `world` ranks by their measured wave times (`contiguous_tiles`
     for mode "cut", `balanced_tiles` for "deal"), then take out of every rank's list the tiles whose
     own wave would last more than `heavy` x a rank's ideal share (total wave time / (slots x world)):
     a launch cannot end before its longest wave, so their pixels are rendered one sample per wave
     (RankPlan.pixels) instead: one sample per wave (split "sample", the measured best), one pixel per wave
-    (RT_RENDER_PIXEL_WAVES, "pixel"), or "auto" (pixel when a tile holds several pixels). world == 1: one plan of every tile, nothing split."""
+    (RT_RENDER_PIXEL_WAVES, "pixel"), or "auto" (pixel when a tile holds several pixels). world == 1: one plan of every tile, nothing split.
+    weights: per-tile factors of the cut (rt_group_rebalance's measured rank speeds)."""
     import numpy as np
 
     c = np.asarray(costs, dtype=np.float64)
-    parts = (contiguous_tiles if mode == "cut" else balanced_tiles)(c, world)
+    parts = contiguous_tiles(c, world, weights) if mode == "cut" else balanced_tiles(c, world)
     if world == 1:
         return [RankPlan(parts[0], [])]
     thr = heavy * c.sum() / (slots * world)

@@ -53,7 +53,8 @@ EXPORTS = ["rt_abi_version", "rt_build_id", "rt_last_error", "rt_device_count", 
            # ABI 6: the multi-GPU frame (rt_group_*), the kernel variants
            "rt_render_variant", "rt_rank_plan", "rt_group_unique_id", "rt_group_create", "rt_group_create_rank", "rt_group_render",
            "rt_group_sync", "rt_group_render_host", "rt_group_frame", "rt_group_info", "rt_group_plan",
-           "rt_group_rank_pixels", "rt_group_kernel_ms", "rt_group_time_rank", "rt_group_count", "rt_group_destroy"]
+           "rt_group_rank_pixels", "rt_group_kernel_ms", "rt_group_time_rank", "rt_group_count", "rt_group_rebalance",
+           "rt_group_destroy"]
 
 _lib = None
 
@@ -126,7 +127,8 @@ def lib():
         L.rt_scene_save_name.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
         if hasattr(L, "rt_group_create"):  # ABI >= 6
             vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
-            L.rt_rank_plan.argtypes = [vp, i32, i32, dbl, i32, vp, vp]
+            L.rt_rank_plan.argtypes = [vp, vp, i32, i32, dbl, i32, vp, vp]
+            L.rt_group_rebalance.argtypes = [vp, i32, i32, vp]
             L.rt_render_variant.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                                             ctypes.POINTER(ctypes.c_uint32)]
             L.rt_group_unique_id.argtypes = [vp, i32]
@@ -191,15 +193,17 @@ def photon_kdtree(pos) -> np.ndarray:
     return out
 
 
-def rank_plan(cost, world: int, heavy: float = 0.0, slots: int = 0):
+def rank_plan(cost, world: int, heavy: float = 0.0, slots: int = 0, weight=None):
     """The deterministic multi-GPU plan of a layout's tile costs (rt_rank_plan, host only):
     (owner int32 [ntiles], order int32 [ntiles]) -- owner[t] in [0, world) renders tile t in its wave
-    run, world + r marks one of rank r's split (one sample per wave) tiles; order = dispatch order."""
+    run, world + r marks one of rank r's split (one sample per wave) tiles; order = dispatch order.
+    weight: per-tile cut factors (the runs hold equal sums of cost x weight)."""
     c = np.ascontiguousarray(cost, dtype=np.uint32)
+    w = None if weight is None else np.ascontiguousarray(weight, dtype=np.float64)
     owner = np.zeros(len(c), dtype=np.int32)
     order = np.zeros(len(c), dtype=np.int32)
-    _check(lib().rt_rank_plan(c.ctypes.data, len(c), world, heavy, slots, owner.ctypes.data, order.ctypes.data),
-           "rt_rank_plan")
+    _check(lib().rt_rank_plan(c.ctypes.data, None if w is None else w.ctypes.data, len(c), world, heavy, slots,
+                              owner.ctypes.data, order.ctypes.data), "rt_rank_plan")
     return owner, order
 
 
@@ -307,6 +311,13 @@ class Group:
         _check(lib().rt_group_time_rank(self._h, rank, warmup, iters, ctypes.byref(a), ctypes.byref(b)),
                "rt_group_time_rank")
         return a.value, b.value
+
+    def rebalance(self, rounds: int = 2, iters: int = 5):
+        """Re-cut the plan from measured rank render times (rt_group_rebalance; collective in rank
+        mode); returns the ranks' render ms after the last cut."""
+        out = np.zeros(self.info()["world"], dtype=np.float64)
+        _check(lib().rt_group_rebalance(self._h, rounds, iters, out.ctypes.data), "rt_group_rebalance")
+        return out
 
     def count(self, rank: int) -> dict:
         st = np.zeros(RT_ST_N, dtype=np.uint64)

@@ -333,8 +333,10 @@ typedef struct rt_group rt_group;
    tiles; order[0..ntiles) = every tile in dispatch order (longest first by quarter-octave cost
    bucket, row-major inside a bucket): a rank's run and split tiles are the subsequences of order it
    owns. heavy <= 0: 1.25 (a tile is split when its cost exceeds heavy x total / (slots x world));
-   slots <= 0: 4096 (wave slots of one MI355X at the render kernel's occupancy). */
-int rt_rank_plan(const uint32_t* cost, int ntiles, int world, double heavy, int slots, int32_t* owner, int32_t* order);
+   slots <= 0: 4096 (wave slots of one MI355X at the render kernel's occupancy). weight (may be NULL):
+   per-tile factors of the cut (the runs hold equal sums of cost x weight; rt_group_rebalance). */
+int rt_rank_plan(const uint32_t* cost, const double* weight, int ntiles, int world, double heavy, int slots,
+                 int32_t* owner, int32_t* order);
 /* One process, n ranks: scenes[i] (rt_scene_create / rt_scene_load_cli on its device) is rank i.
    RCCL transport (ncclCommInitAll; one distinct device per rank) unless RT_GROUP_COPY. p: the frame
    (width, height, spp, seed, flags; row fields ignored). Calibrates the layout on scenes[0]. */
@@ -374,6 +376,12 @@ int rt_group_time_rank(rt_group* g, int rank, int warmup, int iters, double* ste
 /* counters (rt_render_count's) of a driven rank's part: its run and its split tiles (counted as tile
    waves; blocking) */
 int rt_group_count(rt_group* g, int rank, uint64_t* stats);
+/* Re-cut the plan from measured rank render times, `rounds` times (collective in rank mode): each
+   round times every rank's render over `iters` frames (one-process groups: one rank at a time), folds
+   each rank's time per unit of predicted cost into its tiles' cut weights and cuts again (split
+   tiles and dispatch order unchanged). rank_ms[world] (may be NULL): the ranks' render times measured
+   after the last cut. */
+int rt_group_rebalance(rt_group* g, int rounds, int iters, double* rank_ms);
 void rt_group_destroy(rt_group* g);
 
 /* Diagnostics: the device's fdlibm sin / cos / asin / acos (the sequences the trace kernels use,

@@ -132,3 +132,22 @@ def test_group_rejects_bad_arguments():
     with rt.Group.create([g], W, H, spp=spp, seed=seed) as grp:  # no RT_GROUP_RGB: no float plane
         with pytest.raises(rt.RTError):
             grp.render_host(W, H, rgb=True)
+
+
+def test_group_rebalance_recuts_and_keeps_the_frame():
+    """rt_group_rebalance: the ranks' measured render times re-cut the plan (the cut moves, the split
+    tiles and the dispatch order stay) and the frame stays the 1-GPU frame bit for bit."""
+    cli, W, H, spp, seed = CASES[0]
+    g = _scene(cli)
+    rgb, argb = g.render(W, H, spp=spp, seed=seed)
+    with rt.Group.create([g] * 4, W, H, spp=spp, seed=seed, rgb=True, copy=True, heavy=0.1, slots=64) as grp:
+        o0, d0 = grp.plan()
+        ms = grp.rebalance(rounds=2, iters=3)
+        o1, d1 = grp.plan()
+        assert len(ms) == 4 and (ms > 0).all()
+        assert np.array_equal(d0, d1) and np.array_equal(o0 >= 4, o1 >= 4)
+        pix = np.concatenate([grp.rank_pixels(r) for r in range(4)])
+        assert np.array_equal(np.sort(pix), np.arange(W * H))
+        c, a = grp.render_host(W, H)
+        assert np.array_equal(a, argb)
+        assert np.array_equal(c.view(np.uint32), rgb.view(np.uint32))

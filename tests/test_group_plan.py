@@ -7,8 +7,8 @@ import pytest
 from distraytracer_old_amd import multigpu, rt
 
 
-def _native_plans(cost, world, tiles_x, tw, th, W, H, heavy=multigpu.HEAVY, slots=multigpu.WAVE_SLOTS):
-    owner, order = rt.rank_plan(cost, world, heavy, slots)
+def _native_plans(cost, world, tiles_x, tw, th, W, H, heavy=multigpu.HEAVY, slots=multigpu.WAVE_SLOTS, weight=None):
+    owner, order = rt.rank_plan(cost, world, heavy, slots, weight)
     o = owner[order]
     out = []
     for r in range(world):
@@ -64,3 +64,23 @@ def test_cost_bucket_matches_dispatch_key():
 def test_rank_plan_rejects_bad_arguments():
     with pytest.raises(rt.RTError):
         rt.rank_plan(np.ones(4, dtype=np.uint32), 0)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_weighted_cut_equals_python(world):
+    """rt_group_rebalance's cut: the runs hold equal sums of cost x weight (per-rank speed factors)."""
+    W, H, tw, th = 256, 130, 2, 2
+    tiles_x = -(-W // tw)
+    n = tiles_x * (-(-H // th))
+    cost = _costs("lognormal", n, seed=world)
+    g = np.random.default_rng(world)
+    weight = np.repeat(g.uniform(0.6, 1.7, world), -(-n // world))[:n]
+    owner, order, nat = _native_plans(cost, world, tiles_x, tw, th, W, H, slots=64, weight=weight)
+    py = multigpu.rank_plans(cost, world, tiles_x, tw, th, W, H, slots=64, weights=weight)
+    for r in range(world):
+        assert np.array_equal(nat[r][0], py[r].tiles), r
+        assert np.array_equal(nat[r][1], py[r].pixels), r
+    # the weights move the cut (and only the cut: the split tiles and the dispatch order are the same)
+    o0, d0 = rt.rank_plan(cost, world, 0.0, 64)
+    assert np.array_equal(d0, order) and np.array_equal(o0 >= world, owner >= world)
+    assert not np.array_equal(o0, owner)

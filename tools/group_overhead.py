@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--rebalance", type=int, default=0, help="rt_group_rebalance rounds before timing")
     ap.add_argument("--out")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime: torch's)
@@ -37,6 +38,9 @@ def main():
     full = g.time_render(W, H, spp=spp, seed=seed, warmup=2, iters=5)
     rows = []
     with rt.Group.create([g] * a.world, W, H, spp=spp, seed=seed, copy=True) as grp:
+        if a.rebalance:
+            ms = grp.rebalance(rounds=a.rebalance, iters=5)
+            print(json.dumps({"rebalanced_rank_ms": ms.tolist()}), flush=True)
         for r in range(a.world):
             run, split = grp.rank_tiles(r)
             step, kern = grp.time_rank(r, warmup=a.warmup, iters=a.iters)
@@ -47,6 +51,7 @@ def main():
     smax = max(x["step_ms"] for x in rows)
     kmax = max(x["kernel_ms"] for x in rows)
     out = {"config": a.config, "workload": f"{cli} {W}x{H} {spp}spp", "world": a.world, "iters": a.iters,
+           "rebalance_rounds": a.rebalance,
            "full_frame_kernel_ms": full, "max_step_ms": smax, "max_kernel_ms": kmax,
            "step_minus_kernel_us": (smax - kmax) * 1e3,
            "emulated_efficiency": full / a.world / smax, "kernel_efficiency": full / a.world / kmax,
