@@ -294,8 +294,8 @@ def main():
         else:
             grp = rt.Group.create([scene], W, H, spp=spp, seed=seed)
         rank_ms_rebalanced = None
-        if world > 1:  # setup: two re-cuts of the plan from the ranks' measured render times (collective)
-            rank_ms_rebalanced = grp.rebalance(rounds=2, iters=5).tolist()
+        if world > 1:  # setup: three re-cuts of the plan from the ranks' measured render times (collective)
+            rank_ms_rebalanced = grp.rebalance(rounds=3, iters=10).tolist()
         run_t, split_t = grp.rank_tiles(rank)
         my_tiles = np.concatenate([run_t, split_t]).astype(np.int32)
         parallelism = ("1 GPU" if world == 1 else

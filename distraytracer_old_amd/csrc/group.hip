@@ -890,9 +890,13 @@ int rt_group_rebalance(rt_group* g, int rounds, int iters, double* rank_ms) {
   int rc;
   for (int round = 0; round <= rounds; ++round) {
     if ((rc = sync_group(g))) return rc;
-    for (GRank& R : g->r) {  // each rank alone (one-process groups share devices)
-      R.timed = 0;
+    for (GRank& R : g->r) {  // each rank alone (one-process groups share devices), after 3 untimed frames
       const bool r0 = R.rank == 0;
+      for (int i = 0; i < 3; ++i)
+        if ((rc = enqueue_render(g, R, r0 ? g->outRgb : R.fRgb, r0 ? g->outArgb : R.fArgb, false))) return rc;
+      GCHK(hipSetDevice(R.dev));
+      GCHK(hipStreamSynchronize(R.st));
+      R.timed = 0;
       for (int i = 0; i < iters; ++i)
         if ((rc = enqueue_render(g, R, r0 ? g->outRgb : R.fRgb, r0 ? g->outArgb : R.fArgb, true))) return rc;
       int fr = 0;
@@ -919,9 +923,9 @@ int rt_group_rebalance(rt_group* g, int rounds, int iters, double* rank_ms) {
     double Tsum = 0, Csum = 0;
     for (int q = 0; q < g->world; ++q) { Tsum += T[q]; Csum += C[q]; }
     if (!(Tsum > 0) || !(Csum > 0)) break;
-    std::vector<double> f(g->world, 1.0);
+    std::vector<double> f(g->world, 1.0);  // damped (^0.75): the measured times carry a few % of noise
     for (int q = 0; q < g->world; ++q)
-      if (C[q] > 0 && T[q] > 0) f[q] = (T[q] / Tsum) / (C[q] / Csum);
+      if (C[q] > 0 && T[q] > 0) f[q] = std::pow((T[q] / Tsum) / (C[q] / Csum), 0.75);
     for (int t = 0; t < g->ntiles; ++t) g->weight[t] *= f[g->owner[t] % g->world];
     if ((rc = make_plan(g, g->cost, g->heavy, g->slots)) || (rc = setup_lists(g))) return rc;
   }

@@ -39,7 +39,7 @@ def main():
     rows = []
     with rt.Group.create([g] * a.world, W, H, spp=spp, seed=seed, copy=True) as grp:
         if a.rebalance:
-            ms = grp.rebalance(rounds=a.rebalance, iters=5)
+            ms = grp.rebalance(rounds=a.rebalance, iters=10)
             print(json.dumps({"rebalanced_rank_ms": ms.tolist()}), flush=True)
         for r in range(a.world):
             run, split = grp.rank_tiles(r)
