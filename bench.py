@@ -342,8 +342,16 @@ def main():
 
     # setup (untimed, like the counting run): a layout's calibration renders ran when the group /
     # renderer was made; ~0.2 s of untimed frames next -- the GPU's clocks ramp over the first launches
+    # Every frame is collective at N > 1, so the ranks agree on the count (max over ranks of
+    # 0.2 s / one frame): a per-rank time bound would leave them on different frames, deadlocked.
     t_warm = time.perf_counter()
-    while time.perf_counter() - t_warm < 0.2:
+    step()
+    drain()
+    n_warm = torch.tensor([min(200, int(0.2 / max(time.perf_counter() - t_warm, 1e-4)))], dtype=torch.int64,
+                          device=coll_dev)
+    if dist:
+        dist.all_reduce(n_warm, op=dist.ReduceOp.MAX)
+    for _ in range(int(n_warm.item())):
         step()
         drain()
     for _ in range(args.warmup):
