@@ -936,4 +936,57 @@ int rt_group_rebalance(rt_group* g, int rounds, int iters, double* rank_ms) {
 
 void rt_group_destroy(rt_group* g) { (void)destroy_group(g); }
 
+int rt_group_rccl_selftest(int device, int n) {
+  if (n < 1) return set_error(RT_E_INVALID, "rt_group_rccl_selftest: n < 1");
+  int rc = rccl_load();
+  if (rc) return rc;
+  GCHK(hipSetDevice(device));
+  std::vector<int32_t> h(n), back(4 * (size_t)n, 0);
+  for (int i = 0; i < n; ++i) h[i] = (int32_t)(0x9E3779B9u * (uint32_t)(i + 1));
+  int32_t* d = nullptr;  // [0, n) source, [n, 2n) broadcast, [2n, 3n) all-gather, [3n, 4n) received
+  hipStream_t st = nullptr;
+  ncclComm_t c1 = nullptr, c2 = nullptr;
+  std::string err;
+  auto hfail = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && err.empty()) err = std::string(what) + ": " + hipGetErrorString(e);
+    return e != hipSuccess;
+  };
+  auto nfail = [&](ncclResult_t r, const char* what) {
+    if (r != ncclSuccess && err.empty()) err = std::string(what) + ": " + g_rccl.errStr(r);
+    return r != ncclSuccess;
+  };
+  do {
+    if (hfail(hipMalloc(&d, 4 * sizeof(int32_t) * n), "hipMalloc")) break;
+    if (hfail(hipMemset(d + n, 0, 3 * sizeof(int32_t) * n), "hipMemset")) break;
+    if (hfail(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate")) break;
+    if (hfail(hipMemcpy(d, h.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice), "hipMemcpy")) break;
+    ncclUniqueId u;
+    if (nfail(g_rccl.getUniqueId(&u), "ncclGetUniqueId")) break;
+    if (nfail(g_rccl.commInitRank(&c1, 1, u, 0), "ncclCommInitRank")) break;
+    int dev = device;
+    if (nfail(g_rccl.commInitAll(&c2, 1, &dev), "ncclCommInitAll")) break;
+    if (nfail(g_rccl.bcast(d, d + n, (size_t)n, ncclInt32, 0, c1, st), "ncclBroadcast")) break;
+    if (nfail(g_rccl.allGather(d, d + 2 * n, (size_t)n, ncclInt32, c2, st), "ncclAllGather")) break;
+    if (nfail(g_rccl.groupStart(), "ncclGroupStart")) break;
+    ncclResult_t r1 = g_rccl.send(d, (size_t)n, ncclInt32, 0, c1, st);
+    ncclResult_t r2 = g_rccl.recv(d + 3 * n, (size_t)n, ncclInt32, 0, c1, st);
+    ncclResult_t r3 = g_rccl.groupEnd();
+    if (nfail(r1, "ncclSend") || nfail(r2, "ncclRecv") || nfail(r3, "ncclGroupEnd")) break;
+    if (hfail(hipStreamSynchronize(st), "hipStreamSynchronize")) break;
+    if (hfail(hipMemcpy(back.data(), d, 4 * sizeof(int32_t) * n, hipMemcpyDeviceToHost), "hipMemcpy")) break;
+    for (int k = 1; k < 4 && err.empty(); ++k)
+      for (int i = 0; i < n; ++i)
+        if (back[(size_t)k * n + i] != h[i]) {
+          static const char* what[4] = {"", "ncclBroadcast", "ncclAllGather", "ncclSend / ncclRecv"};
+          err = std::string(what[k]) + ": element " + std::to_string(i) + " differs";
+          break;
+        }
+  } while (false);
+  if (c1) (void)g_rccl.commDestroy(c1);
+  if (c2) (void)g_rccl.commDestroy(c2);
+  if (st) (void)hipStreamDestroy(st);
+  if (d) (void)hipFree(d);
+  return err.empty() ? RT_OK : set_error(RT_E_HIP, "rt_group_rccl_selftest: " + err);
+}
+
 }  // extern "C"

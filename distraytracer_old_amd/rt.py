@@ -54,7 +54,7 @@ EXPORTS = ["rt_abi_version", "rt_build_id", "rt_last_error", "rt_device_count", 
            "rt_render_variant", "rt_rank_plan", "rt_group_unique_id", "rt_group_create", "rt_group_create_rank", "rt_group_render",
            "rt_group_sync", "rt_group_render_host", "rt_group_frame", "rt_group_info", "rt_group_plan",
            "rt_group_rank_pixels", "rt_group_kernel_ms", "rt_group_time_rank", "rt_group_count", "rt_group_rebalance",
-           "rt_group_destroy"]
+           "rt_group_destroy", "rt_group_rccl_selftest"]
 
 _lib = None
 
@@ -148,6 +148,7 @@ def lib():
             L.rt_group_count.argtypes = [vp, i32, vp]
             L.rt_group_destroy.argtypes = [vp]
             L.rt_group_destroy.restype = None
+            L.rt_group_rccl_selftest.argtypes = [i32, i32]
         _lib = L
     return _lib
 
@@ -214,6 +215,12 @@ def group_unique_id() -> bytes:
     if n < 0:
         raise RTError(f"rt_group_unique_id failed ({n}): {lib().rt_last_error().decode()}")
     return buf.raw[:n]
+
+
+def rccl_selftest(device: int = 0, n: int = 4099) -> None:
+    """rt_group_rccl_selftest: every RCCL call of the group's transport through a one-rank
+    communicator on `device` (bindings check for one-GPU machines); raises RTError on a failure."""
+    _check(lib().rt_group_rccl_selftest(device, n), "rt_group_rccl_selftest")
 
 
 GROUP_RGB = 1  # RT_GROUP_RGB: exchange the float-RGB plane too

@@ -383,6 +383,12 @@ int rt_group_count(rt_group* g, int rank, uint64_t* stats);
    after the last cut. */
 int rt_group_rebalance(rt_group* g, int rounds, int iters, double* rank_ms);
 void rt_group_destroy(rt_group* g);
+/* Diagnostics: every RCCL entry point the group resolves at run time, called on `device` through a
+   one-rank communicator -- ncclCommInitRank and ncclCommInitAll, ncclBroadcast, ncclAllGather and a
+   grouped ncclSend / ncclRecv to itself of n int32 -- with the data checked on the host. A one-GPU
+   machine cannot run two RCCL ranks (RCCL refuses two ranks on one device), so this is how the
+   transport's bindings are exercised there. Returns RT_OK or an error. */
+int rt_group_rccl_selftest(int device, int n);
 
 /* Diagnostics: the device's fdlibm sin / cos / asin / acos (the sequences the trace kernels use,
    shared bit for bit with the CPU oracle) of x[0..n) into out[4*i .. 4*i+3], host buffers. */

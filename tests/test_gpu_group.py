@@ -151,3 +151,12 @@ def test_group_rebalance_recuts_and_keeps_the_frame():
         c, a = grp.render_host(W, H)
         assert np.array_equal(a, argb)
         assert np.array_equal(c.view(np.uint32), rgb.view(np.uint32))
+
+
+def test_rccl_transport_bindings_on_one_device():
+    """The RCCL entry points the group resolves at run time (dlopen), each called through a one-rank
+    communicator -- init by rank and by device list, broadcast, all-gather, grouped send / receive to
+    itself -- with the data checked. RCCL refuses two ranks on one device, so this one-GPU check is
+    what covers the bindings before the driver's multi-GPU run; the exchange logic itself is covered
+    by the COPY-transport emulation above."""
+    rt.rccl_selftest(0, 4099)
