@@ -101,6 +101,9 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "reslds": [],                              # a finished sample's colour waits in LDS, not in spilled VGPRs
     "reslds0": ["RT_RES_LDS=0"],
     "inner0": ["RT_KNN_INNER=0"],             # the kNN final pass scans every photon below the window (round 4)
+    "sprim0": ["RT_SPRIM=0"],                 # top-level implicit primitives as vector loads (round 4)
+    "sprim1": ["RT_SPRIM=1"],                 # ... as scalar loads in the variants without a photon map
+    "sprim2": ["RT_SPRIM=2"],                 # ... in every variant
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
