@@ -332,28 +332,51 @@ DEVI bool tri_test(const TR& T, V o, V d, double& t, int& st, const LIM& lim = L
   return planar_test<3, false>(T.v, nA, nB, T.dA, T.dB, o, d, t, st, lim);
 }
 
+// SL: the primitive record sits at a wave-uniform address (the packet kernels' top-level scans) and
+// is read with scalar loads into SGPRs instead of one vector load per lane (prim_test<true>)
+template <bool SL, class T>
+DEVI T pld(const T* p) {
+  if constexpr (SL) return *(const __attribute__((address_space(4))) T*)p;
+  else return *p;
+}
+template <bool SL>
+DEVI V pld3(const double* p) { return mk(pld<SL>(p), pld<SL>(p + 1), pld<SL>(p + 2)); }
+
+template <bool SL = false>
 DEVI V sphere_center(const PrimD& P, const Key& k) {
-  if (P.type != PT_MSPHERE) return ld3(P.a);
+  if (pld<SL>(&P.type) != PT_MSPHERE) return pld3<SL>(P.a);
   // myMovingSphere.getOrigin(ray.getTime()) : keyed per (ray, object)
-  double tm = rng(k.seed, k.pixel, k.sample, k.node, k.tsite, P.key, 0, 1.0);
-  V o0 = ld3(P.a), o1 = ld3(P.a + 6);
+  double tm = rng(k.seed, k.pixel, k.sample, k.node, k.tsite, pld<SL>(&P.key), 0, 1.0);
+  V o0 = pld3<SL>(P.a), o1 = pld3<SL>(P.a + 6);
   V bMa = sub(o1, o0);
   return mk(o0.x + tm * bMa.x, o0.y + tm * bMa.y, o0.z + tm * bMa.z);
 }
 
+template <bool SL = false>
 DEVI bool prim_test(const PrimD& P, V o, V d, const Key& k, double& t, int& args) {
-  switch (P.type) {
+  const int32_t type = pld<SL>(&P.type);
+  auto A = [&](int i) { return pld<SL>(P.a + i); };
+  switch (type) {
     case PT_QUAD:
     case PT_PLANE: {
-      const double(*v)[3] = (const double(*)[3])P.a;
-      if (P.type == PT_PLANE)
-        return planar_test<4, true>(v, ld3(P.a + 12), ld3(P.a + 15), P.a[18], P.a[19], o, d, t, args);
-      return planar_test<4, false>(v, ld3(P.a + 12), ld3(P.a + 15), P.a[18], P.a[19], o, d, t, args);
+      if constexpr (SL) {
+        double q[4][3];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) q[i / 3][i % 3] = A(i);
+        if (type == PT_PLANE)
+          return planar_test<4, true>(q, pld3<SL>(P.a + 12), pld3<SL>(P.a + 15), A(18), A(19), o, d, t, args);
+        return planar_test<4, false>(q, pld3<SL>(P.a + 12), pld3<SL>(P.a + 15), A(18), A(19), o, d, t, args);
+      } else {
+        const double(*v)[3] = (const double(*)[3])P.a;
+        if (type == PT_PLANE)
+          return planar_test<4, true>(v, ld3(P.a + 12), ld3(P.a + 15), P.a[18], P.a[19], o, d, t, args);
+        return planar_test<4, false>(v, ld3(P.a + 12), ld3(P.a + 15), P.a[18], P.a[19], o, d, t, args);
+      }
     }
     case PT_SPHERE:
     case PT_MSPHERE: {  // mySphere.intersectCheck (myImpObject.java:76-94)
-      V c = sphere_center(P, k);
-      double rx = P.a[3], ry = P.a[4], rz = P.a[5];
+      V c = sphere_center<SL>(P, k);
+      double rx = A(3), ry = A(4), rz = A(5);
       double a = ((d.x / rx) * (d.x / rx)) + ((d.y / ry) * (d.y / ry)) + ((d.z / rz) * (d.z / rz));
       V pC = mk((o.x - c.x) / rx, (o.y - c.y) / ry, (o.z - c.z) / rz);
       double ta = 2 * a;
@@ -374,8 +397,8 @@ DEVI bool prim_test(const PrimD& P, V o, V d, const Key& k, double& t, int& args
     }
     case PT_CYL:
     case PT_HCYL: {
-      double rx = P.a[3], rz = P.a[4], yTop = P.a[6], yBot = P.a[7];
-      V org = ld3(P.a);
+      double rx = A(3), rz = A(4), yTop = A(6), yBot = A(7);
+      V org = pld3<SL>(P.a);
       double a = ((d.x / rx) * (d.x / rx)) + ((d.z / rz) * (d.z / rz));
       double px = (o.x - org.x) / rx, pz = (o.z - org.z) / rz;
       double b = 2 * (((d.x / rx) * px) + ((d.z / rz) * pz));
@@ -384,7 +407,7 @@ DEVI bool prim_test(const PrimD& P, V o, V d, const Key& k, double& t, int& args
       if (discr < 0) return false;
       double d1 = sqrt(discr), t1 = (-b + d1) / (2 * a), t2 = (-b - d1) / (2 * a);
       double cv = jmin(t1, t2), co = jmax(t1, t2);
-      if (P.type == PT_HCYL) {  // myHollow_Cylinder.intersectCheck :174-192
+      if (type == PT_HCYL) {  // myHollow_Cylinder.intersectCheck :174-192
         if (cv < -EPS) {
           double tmp = co; co = cv; cv = tmp;
           if (cv < -EPS) return false;
@@ -405,10 +428,10 @@ DEVI bool prim_test(const PrimD& P, V o, V d, const Key& k, double& t, int& args
       double pl[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const double* cap = P.a + 8 + 4 * i;
-        double den = cap[0] * d.x + cap[1] * d.y + cap[2] * d.z;
+        const double c0 = A(8 + 4 * i), c1 = A(9 + 4 * i), c2 = A(10 + 4 * i), c3 = A(11 + 4 * i);
+        double den = c0 * d.x + c1 * d.y + c2 * d.z;
         if (fabs(den) > EPS) {
-          double nm = cap[0] * o.x + cap[1] * o.y + cap[2] * o.z + cap[3];
+          double nm = c0 * o.x + c1 * o.y + c2 * o.z + c3;
           pl[i] = -nm / den;
         } else {
           pl[i] = 10000;
@@ -433,9 +456,18 @@ DEVI bool prim_test(const PrimD& P, V o, V d, const Key& k, double& t, int& args
     }
     case PT_BOX: {  // myRndrdBox -> myBBox.intersectCheck
       double te;
-      if (!slab(P.a, P.a + 3, o, d, te)) return false;
-      t = te;
-      args = slab_plane(P.a, P.a + 3, o, d);
+      if constexpr (SL) {
+        double bx[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) bx[i] = A(i);
+        if (!slab(bx, bx + 3, o, d, te)) return false;
+        t = te;
+        args = slab_plane(bx, bx + 3, o, d);
+      } else {
+        if (!slab(P.a, P.a + 3, o, d, te)) return false;
+        t = te;
+        args = slab_plane(P.a, P.a + 3, o, d);
+      }
       return true;
     }
   }

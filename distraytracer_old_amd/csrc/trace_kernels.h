@@ -62,6 +62,16 @@ struct HitCtx {
   do {                                                                                    \
     if (CNT && __lane_id() == (int)__builtin_ctzll(__ballot(1))) ct.c[idx] += (n);        \
   } while (0)
+// Implicit primitives at a wave-uniform address (the packet kernels' top-level scans) as scalar loads
+// into SGPRs: the record no longer occupies VGPRs inside C4's shadow scan, whose reloads of spilled
+// values in that loop went from 21 static scratch ops to 1 (C4 469.5 -> 454.4 ms, C5 195.3 -> 195.1 ms,
+// same images: profiles/r05h_sprim_ab.log). RT_SPRIM 2 = every variant, 1 = the variants without a
+// photon map, 0 = none (vector loads, one per lane)
+#ifndef RT_SPRIM
+#define RT_SPRIM 2
+#endif
+template <uint32_t F>
+static constexpr bool SPRIM = RT_SPRIM == 2 || (RT_SPRIM == 1 && (F & FT_PHOTON) == 0);
 // WAVE: the record address is wave-uniform (counted once per wave step), else per lane
 template <bool CNT, uint32_t F, class LIM = LimNone, bool WAVE = false>
 DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, double& t, int& args, Counters& ct,
@@ -77,7 +87,7 @@ DEVI bool test_ref(const SceneD& S, int32_t ref, V o, V d, const Key& k, double&
     ct.c[c]++;
     if (WAVE) WCNT(c + (C_WQUAD - C_QUAD), 1); else ct.c[c + (C_WQUAD - C_QUAD)]++;
   }
-  return prim_test(P, o, d, k, t, args);
+  return prim_test<WAVE && SPRIM<F>>(P, o, d, k, t, args);
 }
 template <uint32_t F>
 DEVI int32_t ref_xf(const SceneD& S, int32_t ref) { return (!(F & FT_PRIM) || ref >= 0) ? S.tri[ref].xf : S.prim[~ref].xf; }
