@@ -67,6 +67,12 @@ struct HitCtx {
 // values in that loop went from 21 static scratch ops to 1 (C4 469.5 -> 454.4 ms, C5 195.3 -> 195.1 ms,
 // same images: profiles/r05h_sprim_ab.log). RT_SPRIM 2 = every variant, 1 = the variants without a
 // photon map, 0 = none (vector loads, one per lane)
+// RT_ULOAD: other wave-uniform records read in hot loops as scalar loads -- bit 0: a leaf member's
+// transform inverse in the packet traversals (C3 3.069 -> 3.056 ms, C4 unchanged), bit 1: the light
+// record's spot / disk fields in light_sum (C4 456 -> 476 ms: off). profiles/r05i_uload_ab.log
+#ifndef RT_ULOAD
+#define RT_ULOAD 1
+#endif
 #ifndef RT_SPRIM
 #define RT_SPRIM 2
 #endif
@@ -260,7 +266,11 @@ DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRa
     int xf = ref_xf_u<F, PK>(S, ref);
     V o, d;
     if (xf == accXf && !w.moved) { o = ao; d = ad; }
-    else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
+    else if (PK && (RT_ULOAD & 1)) {  // xf is wave-uniform here (ref_xf_u): the inverse as scalar loads
+      double inv[12];
+      sload_inv(S.xf + xf, inv);
+      o = xpt(inv, w.o); d = xvec(inv, w.d);
+    } else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
     double t;
     int args;
     if (test_ref_u<CNT, F, PK>(S, ref, o, d, k, t, args, ct, LimClosest{local, best.t})) {
@@ -979,7 +989,11 @@ DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w
     int xf = ref_xf_u<F, PK>(S, ref);
     V o, d;
     if (xf == accXf && !w.moved) { o = ao; d = ad; }
-    else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
+    else if (PK && (RT_ULOAD & 1)) {  // xf is wave-uniform here (ref_xf_u): the inverse as scalar loads
+      double inv[12];
+      sload_inv(S.xf + xf, inv);
+      o = xpt(inv, w.o); d = xvec(inv, w.d);
+    } else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
     double t;
     int args;
     if (test_ref_u<CNT, F, PK>(S, ref, o, d, k, t, args, ct, LimShadow{dist}) && (dist - t) > EPS) return true;
@@ -2289,12 +2303,15 @@ DEVI V rot_axis(V v1, V u, double thet) {  // rotVecAroundAxis (DistRayTracer.ja
             (uxyC1 + uzS) * v1.x + (uy2 * oneMC + cT) * v1.y + (uyzC1 - uxS) * v1.z,
             (uxzC1 - uyS) * v1.x + (uyzC1 + uxS) * v1.y + (uz2 * oneMC + cT) * v1.z);
 }
+// U: L is wave-uniform (light_sum's loop): its fields as scalar loads
+template <bool U = false>
 DEVI V disk_pos(const LightD& L, const Key& k, uint32_t kk) {  // getRandomDiskPos (myLight.java:251-258)
-  double th = rng(k.seed, k.pixel, k.sample, k.node, SITE_DISK + L.index, kk, 0, TWO_PI_F);
-  V r = nrmz(rot_axis(ld3(L.tangent), ld3(L.orient), th));
-  double m = rng(k.seed, k.pixel, k.sample, k.node, SITE_DISK + L.index, kk + 1, 0, L.radius);
+  const int32_t li = pld<U>(&L.index);
+  double th = rng(k.seed, k.pixel, k.sample, k.node, SITE_DISK + li, kk, 0, TWO_PI_F);
+  V r = nrmz(rot_axis(pld3<U>(L.tangent), pld3<U>(L.orient), th));
+  double m = rng(k.seed, k.pixel, k.sample, k.node, SITE_DISK + li, kk + 1, 0, pld<U>(&L.radius));
   r = mk(r.x * m, r.y * m, r.z * m);
-  return mk(r.x + L.origin[0], r.y + L.origin[1], r.z + L.origin[2]);
+  return mk(r.x + pld<U>(L.origin), r.y + pld<U>(L.origin + 1), r.z + pld<U>(L.origin + 2));
 }
 
 // calcShadowColor (myObjShader.java:98-153)
@@ -2335,7 +2352,7 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     const V lorg = mk(sload(L.origin), sload(L.origin + 1), sload(L.origin + 2));
     const V lcol = mk(sload(L.color), sload(L.color + 1), sload(L.color + 2));
     const bool disk = (F & FT_LIGHTX) && ltype == 2;
-    V lo = disk ? disk_pos(L, k, 0) : lorg;
+    V lo = disk ? disk_pos<(RT_ULOAD & 2) != 0>(L, k, 0) : lorg;
     V ln = xpt(lg, lo);
     ln = nrmz(mk(ln.x - h.fwd.x, ln.y - h.fwd.y, ln.z - h.fwd.z));
     WRay sr;
@@ -2345,14 +2362,16 @@ DEVI V light_sum(const SceneD& S, const MatD& m, const HitRec& h, V tex, const K
     sr.stable = false;
     sr.moved = false;
     sr.ver = 0;
-    V lo2 = disk ? disk_pos(L, k, 2) : lorg;
+    V lo2 = disk ? disk_pos<(RT_ULOAD & 2) != 0>(L, k, 2) : lorg;
     double t = sqrt((((sr.o.x - lo2.x) * (sr.o.x - lo2.x)) + ((sr.o.y - lo2.y) * (sr.o.y - lo2.y))) + ((sr.o.z - lo2.z) * (sr.o.z - lo2.z)));
     double ltMult = 1;
     if (CNT) ct.c[C_LIGHT]++;
     WCNT(C_WLIGHT, 1);  // the light record: scalar loads, once per wave
     if ((F & FT_LIGHTX) && ltype == 1) {  // mySpotLight.intersectCheck / calcT_Mult (myLight.java:77-82,159-163)
-      double angle = jf::acos(-1 * dot(sr.d, ld3(L.orient)));
-      ltMult = (angle < L.innerRad) ? 1 : (angle > L.outerRad) ? 0 : (L.outerRad - angle) / L.radDiff;
+      constexpr bool U = (RT_ULOAD & 2) != 0;
+      double angle = jf::acos(-1 * dot(sr.d, pld3<U>(L.orient)));
+      const double inR = pld<U>(&L.innerRad), outR = pld<U>(&L.outerRad);
+      ltMult = (angle < inR) ? 1 : (angle > outR) ? 0 : (outR - angle) / pld<U>(&L.radDiff);
     }
     if (ltMult == 0) continue;
     if (CNT) ct.c[C_SHADOW]++;
@@ -2808,18 +2827,19 @@ DEVI ShRay shadow_ray(const SceneD& S, int li, V fwd, const Key& k) {
   for (int q = 0; q < 12; ++q) lg[q] = ld(L.g + q);
   const V lorg = mk(ld(L.origin), ld(L.origin + 1), ld(L.origin + 2));
   const bool disk = (F & FT_LIGHTX) && ltype == 2;
-  const V lo = disk ? disk_pos(L, k, 0) : lorg;
+  const V lo = disk ? disk_pos<U>(L, k, 0) : lorg;
   V ln = xpt(lg, lo);
   ln = nrmz(mk(ln.x - fwd.x, ln.y - fwd.y, ln.z - fwd.z));
   ShRay r;
   r.d = nrmz(ln);  // myRay ctor normalises again
-  const V lo2 = disk ? disk_pos(L, k, 2) : lorg;
+  const V lo2 = disk ? disk_pos<U>(L, k, 2) : lorg;
   r.dist = sqrt((((fwd.x - lo2.x) * (fwd.x - lo2.x)) + ((fwd.y - lo2.y) * (fwd.y - lo2.y))) +
                 ((fwd.z - lo2.z) * (fwd.z - lo2.z)));
   r.ltm = 1;
   if ((F & FT_LIGHTX) && ltype == 1) {  // mySpotLight.calcT_Mult (myLight.java:77-82,159-163)
-    const double angle = jf::acos(-1 * dot(r.d, ld3(L.orient)));
-    r.ltm = (angle < L.innerRad) ? 1 : (angle > L.outerRad) ? 0 : (L.outerRad - angle) / L.radDiff;
+    const double angle = jf::acos(-1 * dot(r.d, pld3<U>(L.orient)));
+    const double inR = pld<U>(&L.innerRad), outR = pld<U>(&L.outerRad);
+    r.ltm = (angle < inR) ? 1 : (angle > outR) ? 0 : (outR - angle) / pld<U>(&L.radDiff);
   }
   return r;
 }

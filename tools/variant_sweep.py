@@ -104,6 +104,10 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "sprim0": ["RT_SPRIM=0"],                 # top-level implicit primitives as vector loads (round 4)
     "sprim1": ["RT_SPRIM=1"],                 # ... as scalar loads in the variants without a photon map
     "sprim2": ["RT_SPRIM=2"],                 # ... in every variant
+    "uload0": ["RT_ULOAD=0"],                 # leaf transforms / light fields as per-lane loads
+    "uload1": ["RT_ULOAD=1"],                 # the leaf member's transform inverse as scalar loads
+    "uload2": ["RT_ULOAD=2"],                 # the light's spot / disk fields as scalar loads
+    "uload3": ["RT_ULOAD=3"],
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
