@@ -1873,10 +1873,23 @@ DEVI void photon_scan_any(const SceneD& S, const double* pos, double R2, Counter
 // largest d^2 as the heap; the powers are summed in scan order rather than the
 // reference's poll order (a last-ulp difference; DESIGN.md "Precision").
 // Start window: [0, R2) with R2 from the local density of the smallest photon-BVH node
-// around p holding >= k photons; if fewer than k photons fall below it, the next try is
-// that node's far-corner distance (all its photons lie within it), then max_dist^2.
+// around p holding >= k photons; if fewer than k photons fall below it, the next window starts
+// there and extends by the density extrapolation, capped at that node's far-corner distance (all
+// its photons lie within it), then max_dist^2.
 #ifndef RT_KNN_SHELL
 #define RT_KNN_SHELL 10
+#endif
+// A start window holding fewer than K photons (all of them in the set) is widened by the
+// surface-density extrapolation of what is missing (count ~ d^2: hi x START x K / count), the new
+// window starting above the counted photons, instead of straight to the enclosing node's far corner
+// -- whose wide buckets then needed further passes. With that cheap recovery a tighter start window
+// pays: C5 193.4 -> 179.1 ms at START 1.15 (1.0 / 1.1 / 1.2 / 1.25 / 1.3: 251 / 180.4 / 180.5 / 183.0 /
+// 186.0 ms), the same k-sets and the same image bit for bit (profiles/r05j_*, r05k_*).
+#ifndef RT_KNN_EXTRAP
+#define RT_KNN_EXTRAP 1
+#endif
+#ifndef RT_KNN_START  // the start window: this many times the d^2 holding K photons at the node's density
+#define RT_KNN_START 1.15
 #endif
 #ifndef RT_KNN_EDGES
 #define RT_KNN_EDGES 16
@@ -2095,7 +2108,7 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
           R2far = fmin(R2max, far2 * (1 + 0x1p-40));
           // photons lie on surfaces: density over the box's two largest extents
           const double a = fmax(fmax(e[0] * e[1], e[0] * e[2]), e[1] * e[2]);
-          R2dens = fmin(R2far, 1.3 * K * a / (PI_D * nd.padR[1]));
+          R2dens = fmin(R2far, RT_KNN_START * K * a / (PI_D * nd.padR[1]));
         }
         break;
       }
@@ -2159,7 +2172,16 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
     PROF_CNT(R_KNN_NPASS);
     if ((int)total < K) {  // only possible for the start window: widen it
       if (hi == R2max) { all = true; break; }
+#if RT_KNN_EXTRAP
+      // every photon under hi is in the set: the window moves above it, and grows by the
+      // surface-density extrapolation (count ~ d^2) of what is still missing, at most to R2far
+      const double ext = total > 0 ? hi * (RT_KNN_START * K / (double)total) : R2far;
+      lo = hi;
+      below = (int)total;
+      hi = (hi < R2far) ? fmin(R2far, ext) : R2max;
+#else
       hi = (hi < R2far) ? R2far : R2max;
+#endif
       continue;
     }
     // the window becomes [e[kb - 1], e[kb]) with e[k] = lo + (k + 1) w, e[ne - 1] = hi (the

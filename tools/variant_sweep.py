@@ -108,6 +108,13 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "uload1": ["RT_ULOAD=1"],                 # the leaf member's transform inverse as scalar loads
     "uload2": ["RT_ULOAD=2"],                 # the light's spot / disk fields as scalar loads
     "uload3": ["RT_ULOAD=3"],
+    "ex0": ["RT_KNN_EXTRAP=0"],               # kNN start window too small: widen to the node's far corner
+    "ex1": ["RT_KNN_EXTRAP=1"],               # ... to the density extrapolation, above the counted photons
+    "ex1s115": ["RT_KNN_EXTRAP=1", "RT_KNN_START=1.15"],
+    "ex1s10": ["RT_KNN_EXTRAP=1", "RT_KNN_START=1.0"],
+    "ex1s11": ["RT_KNN_EXTRAP=1", "RT_KNN_START=1.1"],
+    "ex1s12": ["RT_KNN_EXTRAP=1", "RT_KNN_START=1.2"],
+    "ex1s125": ["RT_KNN_EXTRAP=1", "RT_KNN_START=1.25"],
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
@@ -137,13 +144,16 @@ def do_build(names):
             print("built", p, flush=True)
 
 
-def time_one(cfg: str, W: int, H: int, spp: int, iters: int, flags: int):
+def time_one(cfg: str, W: int, H: int, spp: int, iters: int, flags: int, save: str = ""):
     from distraytracer_old_amd import rt, scenes
     cli, W0, H0, spp0, seed = scenes.CONFIGS[cfg]
     scenes.ensure_bun69k()
     with rt.Scene.load_cli(cli, textures=scenes.prepare(cli)) as s:
         W = W or W0; H = H or H0; spp = spp or spp0
-        _, argb = s.render(W, H, spp=spp, seed=seed, flags=flags)
+        rgb, argb = s.render(W, H, spp=spp, seed=seed, flags=flags)
+        if save:  # the frame, to compare builds whose images may differ in the last bits
+            import numpy as np
+            np.savez_compressed(save, rgb=rgb, argb=argb)
         ms = s.time_render(W, H, spp=spp, seed=seed, warmup=1, iters=iters, flags=flags)
     return {"ms": ms, "hash": hashlib.sha1(argb.tobytes()).hexdigest()[:12], "W": W, "H": H, "spp": spp}
 
@@ -159,18 +169,22 @@ def main():
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--flags", type=int, default=0)
+    ap.add_argument("--save", default="", help="directory: each build's frame as <name>_<cfg>.npz")
     a = ap.parse_args()
     names = a.names.split(",")
     if a.mode == "build":
         do_build(names)
     elif a.mode == "one":
-        print(json.dumps(time_one(a.cfg, a.W, a.H, a.spp, a.iters, a.flags)))
+        print(json.dumps(time_one(a.cfg, a.W, a.H, a.spp, a.iters, a.flags, a.save)))
     else:
         for n in names:
             lib = OUT / f"lib_{n}.so"
             env = dict(os.environ, DISTRAYTRACER_LIB=str(lib))
             cmd = [sys.executable, __file__, "one", "--cfg", a.cfg, "--W", str(a.W), "--H", str(a.H), "--spp", str(a.spp),
                    "--iters", str(a.iters), "--flags", str(a.flags)]
+            if a.save:
+                os.makedirs(a.save, exist_ok=True)
+                cmd += ["--save", os.path.join(a.save, f"{n}_{a.cfg}.npz")]
             r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
             line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 and r.stdout.strip() else r.stderr[-800:]
             print(n, a.cfg, line, flush=True)
