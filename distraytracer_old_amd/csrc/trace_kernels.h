@@ -1907,7 +1907,14 @@ static constexpr bool KNN_LDS_HIST = PACKET && RT_KNN_LDS_HIST != 0;
 #define RT_KNN_H16 1
 #endif
 static constexpr bool KNN_H16 = KNN_LDS_HIST && RT_KNN_H16 != 0;
-static constexpr int KNN_HB = KNN_H16 ? 64 : KNN_EDGES;
+// KNN_H8: 128 u8 buckets in the same words, so a pass narrows the window 8x further than 16 u32
+// ones (a carry is detected by the buckets' sum; such a lane repeats the pass with the u16 buckets).
+// Passes per gather call drop, C5 179.9 -> 175.0 ms, same image (profiles/r05n_c5_knn_h8_ab.log).
+#ifndef RT_KNN_H8
+#define RT_KNN_H8 1
+#endif
+static constexpr bool KNN_H8 = KNN_H16 && RT_KNN_H8 != 0;
+static constexpr int KNN_HB = KNN_H8 ? 128 : KNN_H16 ? 64 : KNN_EDGES;
 static_assert(!KNN_LDS_HIST || KNN_SHELL * 64 * 12 <= PK_LDS * 64 * 8, "window list fits the pkT levels");
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // One counting pass over [lo, hi) through a per-lane LDS histogram (packet kernels: the
@@ -1918,17 +1925,20 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // kb = 0) and c(kb). P16: two u16 buckets per LDS word (NB = 64 in the same 8 KB as 16 u32
 // ones, so the first pass narrows 4x further); ovf reports more than 65535 photons below hi,
 // whose counts may have carried between the halves (the caller repeats the pass with u32).
-template <bool CNT, int NB, bool P16>
+template <bool CNT, int NB, bool P16, bool P8 = false>
 DEVI void knn_hist_pass(const SceneD& S, const double* pos, double lo, double hi, int K, Counters& ct,
                         uint32_t& total, int& kb, uint32_t& cPrev, uint32_t& cAt, bool& ovf, bool lw = false) {
-  constexpr int NW = P16 ? NB / 2 : NB;  // LDS words per lane
+  constexpr int NW = P8 ? NB / 4 : P16 ? NB / 2 : NB;  // LDS words per lane
   static_assert(NW * 64 * 4 <= PK_LDS * 64 * 8, "histogram fits the pkT levels");
   lds_u32* hist = (lds_u32*)pkT() + __lane_id();
 #pragma unroll
   for (int q = 0; q < NW; ++q) hist[q * 64] = 0;
   uint32_t tot = 0;
   auto bump = [&](int j) {
-    if (P16) {
+    if (P8) {
+      __hip_atomic_fetch_add(hist + (j >> 2) * 64, 1u << ((j & 3) * 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      tot++;
+    } else if (P16) {
       __hip_atomic_fetch_add(hist + (j >> 1) * 64, 1u << ((j & 1) * 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       tot++;
     } else {
@@ -1955,16 +1965,20 @@ DEVI void knn_hist_pass(const SceneD& S, const double* pos, double lo, double hi
       bump(j);
     }, lw);
   }
-  ovf = P16 && tot > (uint32_t)S.knnU16Max;
+  ovf = (P16 || P8) && tot > (uint32_t)S.knnU16Max;  // (the test knob lowers the u8 pass's limit too)
+  uint32_t sum = 0;
   for (int q = 0; q < NW; ++q) {
     const uint32_t v = hist[q * 64];
 #pragma unroll
-    for (int h = 0; h < (P16 ? 2 : 1); ++h) {
-      const uint32_t run = total + (P16 ? ((v >> (16 * h)) & 0xffffu) : v);
-      if (kb < 0 && (int)run >= K) { kb = P16 ? 2 * q + h : q; cPrev = total; cAt = run; }
+    for (int h = 0; h < (P8 ? 4 : P16 ? 2 : 1); ++h) {
+      const uint32_t c = P8 ? ((v >> (8 * h)) & 0xffu) : P16 ? ((v >> (16 * h)) & 0xffffu) : v;
+      const uint32_t run = total + c;
+      if (P8) sum += c;
+      if (kb < 0 && (int)run >= K) { kb = P8 ? 4 * q + h : P16 ? 2 * q + h : q; cPrev = total; cAt = run; }
       total = run;
     }
   }
+  if (P8 && sum != tot) ovf = true;  // a u8 carry: the buckets' sum falls short by 255 (256 out of a word)
 }
 
 // Exact replay of the reference's neighbourhood for ONE lane whose k-th distance is tied (several
@@ -2141,8 +2155,15 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
     int ne = NE;  // this lane's edges in this pass: e[k] = lo + (k + 1) w, w = (hi - lo) / ne
     if constexpr (KNN_LDS_HIST) {
       bool ovf = false;
-      knn_hist_pass<CNT, KNN_HB, KNN_H16>(S, pos, lo, hi, K, ct, total, kb, cPrev, cAt, ovf, lw);
+      knn_hist_pass<CNT, KNN_HB, KNN_H16 && !KNN_H8, KNN_H8>(S, pos, lo, hi, K, ct, total, kb, cPrev, cAt, ovf, lw);
       ne = KNN_HB;
+      if (KNN_H8 && __ballot(ovf)) {  // a u8 bucket may have carried: this pass again with u16 buckets
+        if (ovf) {
+          total = cPrev = cAt = 0; kb = -1; ovf = false;
+          knn_hist_pass<CNT, 64, true>(S, pos, lo, hi, K, ct, total, kb, cPrev, cAt, ovf, lw);
+          ne = 64;
+        }
+      }
       if (KNN_H16 && __ballot(ovf)) {  // > 65535 photons below hi: this pass again with u32 buckets
         if (ovf) {
           total = cPrev = cAt = 0; kb = -1;
@@ -2186,7 +2207,7 @@ DEVI V irradiance(const SceneD& S, V p, Counters& ct) {
     }
     // the window becomes [e[kb - 1], e[kb]) with e[k] = lo + (k + 1) w, e[ne - 1] = hi (the
     // pass's w: (hi - lo) / ne, an exact power-of-two scaling either way)
-    const double wp = (hi - lo) * (ne == NE ? 1.0 / NE : 1.0 / KNN_HB);
+    const double wp = (hi - lo) * (ne == NE ? 1.0 / NE : ne == 64 ? 1.0 / 64 : 1.0 / 128);
     const double nhi = (kb == ne - 1) ? hi : lo + (kb + 1) * wp;
     const double nlo = kb ? lo + kb * wp : lo;
     const int nbelow = kb ? (int)cPrev : below, cb = (int)cAt;

@@ -146,3 +146,33 @@ def test_gather_ties_at_the_largest_k(tmp_path, seed):
         else:
             np.testing.assert_allclose(gv, ev, rtol=1e-12, atol=0)
     assert ties >= 5
+
+
+def test_gather_u8_bucket_carry_falls_back(tmp_path):
+    """The counting passes keep 128 u8 buckets per lane (KNN_H8); a bucket holding more than 255
+    photons carries into its neighbour, which the pass detects from the buckets' sum and repeats with
+    u16 buckets. 300 photons at distinct distances within 3e-7 of radius 1 around the query points
+    land in one bucket of the first pass: the k = 100 nearest must still be the oracle's."""
+    k = 100
+    cli = tmp_path / "knn.cli"
+    cli.write_text(f"fov 60\nbackground 0 0 0\npoint_light 0 5 0 1 1 1\ndiffuse_photons 100 {k} 100\n"
+                   "diffuse .5 .5 .5 0 0 0\nsphere 1 0 0 -5\n")
+    rng = np.random.default_rng(11)
+    d = rng.normal(size=(300, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    shell = d * (1.0 + np.arange(300)[:, None] * 1e-9)
+    far = rng.normal(size=(60, 3))
+    far *= (2.0 + rng.random((60, 1))) / np.linalg.norm(far, axis=1, keepdims=True)
+    pos = np.concatenate([shell, far])
+    pos = pos[rng.permutation(len(pos))]
+    pwr = rng.random((len(pos), 3))
+    g = rt.Scene.load_cli("knn.cli", scene_dir=tmp_path, textures={})
+    g.set_photons(pos, pwr)
+    o = OracleScene(tmp_path, "knn.cli")
+    o.set_photons(pos, pwr)
+    qs = np.array([(0.0, 0.0, 0.0), (1e-9, 0.0, 0.0), (0.0, -2e-9, 1e-9)])
+    got = g.photon_gather(qs)
+    for q, gv in zip(qs, got):
+        ev, straddle = _oracle_irradiance(o, pos, pwr, q, k)
+        assert not straddle
+        np.testing.assert_allclose(gv, ev, rtol=1e-12, atol=0)

@@ -187,13 +187,14 @@ def test_c5_full_prepass_and_k200_gather_parity():
 
 
 def test_knn_u16_bucket_fallback_renders_identically(monkeypatch):
-    """The kNN counting passes keep 64 u16 buckets per lane and repeat a pass with 16 u32
-    buckets for a lane with more photons below the window's top than the u16 halves hold.
-    DISTRAYTRACER_KNN_U16_MAX (read at scene creation) lowers that threshold to 300, so most
-    first passes of C5's k = 200 gather take the fallback: the image must not change."""
+    """The kNN counting passes keep 128 u8 buckets per lane, repeat a pass with 64 u16 buckets for a
+    lane whose u8 buckets may have carried, and with 16 u32 buckets for a lane with more photons
+    bucketed than the u16 halves hold. DISTRAYTRACER_KNN_U16_MAX (read at scene creation) lowers both
+    limits to 100 photons, so nearly every pass of C5's k = 200 gather takes both fallbacks: the
+    image must not change."""
     seed = 0x5EED0005
     imgs = []
-    for lim in (None, "300"):
+    for lim in (None, "100"):
         if lim:
             monkeypatch.setenv("DISTRAYTRACER_KNN_U16_MAX", lim)
         g = rt.Scene.load_cli("t11.cli", textures={})

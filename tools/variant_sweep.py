@@ -115,6 +115,10 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "ex1s11": ["RT_KNN_EXTRAP=1", "RT_KNN_START=1.1"],
     "ex1s12": ["RT_KNN_EXTRAP=1", "RT_KNN_START=1.2"],
     "ex1s125": ["RT_KNN_EXTRAP=1", "RT_KNN_START=1.25"],
+    "h8off": ["RT_KNN_H8=0"],                 # kNN counting: 64 u16 LDS buckets (round 2)
+    "h8on": ["RT_KNN_H8=1"],                  # 128 u8 buckets, u16 pass on a carry
+    "h8s12": ["RT_KNN_H8=1", "RT_KNN_START=1.2"],
+    "h8s13": ["RT_KNN_H8=1", "RT_KNN_START=1.3"],
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
