@@ -244,20 +244,21 @@ struct rt_group {
   hipEvent_t evRecv[2] = {};    // receive slab b consumed by its scatter
   std::vector<hipEvent_t> evCopied;  // COPY transport: rank r's copy into the slab done
   int64_t frame = 0;
-  std::vector<void*> allocs;
+  std::vector<void*> allocs;      // for the group's life (streams' frames, rank 0's output)
+  std::vector<void*> planAllocs;  // per plan (setup_lists; freed when rt_group_rebalance re-cuts)
 };
 
 namespace {
-int gmalloc(rt_group* g, void** p, size_t bytes) {
+int gmalloc(rt_group* g, void** p, size_t bytes, bool plan = false) {
   *p = nullptr;
   if (bytes == 0) return RT_OK;
   GCHK(hipMalloc(p, bytes));
-  g->allocs.push_back(*p);
+  (plan ? g->planAllocs : g->allocs).push_back(*p);
   return RT_OK;
 }
 template <class T>
-int gupload(rt_group* g, const std::vector<T>& v, T** out) {
-  int rc = gmalloc(g, (void**)out, v.size() * sizeof(T));
+int gupload(rt_group* g, const std::vector<T>& v, T** out) {  // a plan's list
+  int rc = gmalloc(g, (void**)out, v.size() * sizeof(T), true);
   if (rc || v.empty()) return rc;
   GCHK(hipMemcpy(*out, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
   return RT_OK;
@@ -287,6 +288,7 @@ void rank_lists(const rt_group* g, int q, std::vector<int32_t>& tiles, std::vect
 }
 
 int destroy_group(rt_group* g);
+int sync_group(rt_group* g);
 
 // once per group: the per-rank streams and events, rank 0's slab events, the whole-frame buffers
 int setup_streams(rt_group* g) {
@@ -329,6 +331,12 @@ int setup_streams(rt_group* g) {
 // per plan (again after rt_group_rebalance): the ranks' tile / pixel lists on the device, their
 // sample buffers and send slabs, rank 0's scatter list and receive slabs
 int setup_lists(rt_group* g) {
+  if (!g->planAllocs.empty()) {  // a re-cut: the previous plan's buffers, once no stream uses them
+    int rc0 = sync_group(g);
+    if (rc0) return rc0;
+    for (void* p : g->planAllocs) GCHK(hipFree(p));
+    g->planAllocs.clear();
+  }
   g->npix.assign(g->world, 0);
   {
     std::vector<int32_t> a, b, c, d;
@@ -349,11 +357,11 @@ int setup_lists(rt_group* g) {
     if ((rc = gupload(g, R.hTiles, &R.dTiles)) || (rc = gupload(g, R.hPix, &R.dPix)) || (rc = gupload(g, R.hAll, &R.dAll)))
       return rc;
     const size_t ns = R.hPix.size() * (size_t)R.P.spp;
-    if ((rc = gmalloc(g, (void**)&R.smpCol, ns * 3 * sizeof(double))) || (rc = gmalloc(g, (void**)&R.smpTr, ns))) return rc;
+    if ((rc = gmalloc(g, (void**)&R.smpCol, ns * 3 * sizeof(double), true)) || (rc = gmalloc(g, (void**)&R.smpTr, ns, true))) return rc;
     if (R.rank != 0)
       for (int b = 0; b < 2; ++b) {
-        if ((rc = gmalloc(g, (void**)&R.sArgb[b], R.hAll.size() * sizeof(int32_t)))) return rc;
-        if (g->rgb && (rc = gmalloc(g, (void**)&R.sRgb[b], R.hAll.size() * 3 * sizeof(float)))) return rc;
+        if ((rc = gmalloc(g, (void**)&R.sArgb[b], R.hAll.size() * sizeof(int32_t), true))) return rc;
+        if (g->rgb && (rc = gmalloc(g, (void**)&R.sRgb[b], R.hAll.size() * 3 * sizeof(float), true))) return rc;
       }
   }
   if (g->root) {
@@ -368,8 +376,8 @@ int setup_lists(rt_group* g) {
     int rc;
     if ((rc = gupload(g, scat, &g->dScat))) return rc;
     for (int b2 = 0; b2 < 2; ++b2) {
-      if ((rc = gmalloc(g, (void**)&g->rArgb[b2], g->nRecv * sizeof(int32_t)))) return rc;
-      if (g->rgb && (rc = gmalloc(g, (void**)&g->rRgb[b2], g->nRecv * 3 * sizeof(float)))) return rc;
+      if ((rc = gmalloc(g, (void**)&g->rArgb[b2], g->nRecv * sizeof(int32_t), true))) return rc;
+      if (g->rgb && (rc = gmalloc(g, (void**)&g->rRgb[b2], g->nRecv * 3 * sizeof(float), true))) return rc;
     }
   }
   return RT_OK;
@@ -581,6 +589,7 @@ int destroy_group(rt_group* g) {
   for (hipEvent_t e : g->evRecv)
     if (e) (void)hipEventDestroy(e);
   for (void* p : g->allocs) (void)hipFree(p);
+  for (void* p : g->planAllocs) (void)hipFree(p);
   if (g->stage) (void)hipHostFree(g->stage);
   delete g;
   return RT_OK;

@@ -129,7 +129,7 @@ DEVI WfOut wf_shade(const SceneD& S, const Child& in, Key& k, WfNode& rec) {
   FrameOf<F> Fr;
   Child a;
   V loc;
-  const int nch = shade_node<false, F>(S, h, in, k, Fr, loc, a, branch, ct);
+  const int nch = shade_node<false, F, false>(S, h, in, k, Fr, loc, a, branch, ct);  // every frame field
   if (nch == 0) {
     r.c = branch ? clampc(add(loc, mk(0, 0, 0))) : clampc(loc);
     return r;

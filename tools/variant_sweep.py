@@ -119,6 +119,8 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "h8on": ["RT_KNN_H8=1"],                  # 128 u8 buckets, u16 pass on a carry
     "h8s12": ["RT_KNN_H8=1", "RT_KNN_START=1.2"],
     "h8s13": ["RT_KNN_H8=1", "RT_KNN_START=1.3"],
+    "slim0": ["RT_FRAME_SLIM=0"],             # shading-tree frames with every field (round 4)
+    "slim1": ["RT_FRAME_SLIM=1"],             # ... without the fields derivable at the fold
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
