@@ -2549,9 +2549,10 @@ DEVI void kt_of(const SceneD& S, int32_t ktm, double ik[2]) {
 enum : uint8_t { FM_REFL = 0, FM_FRESNEL = 1, FM_SIMPLE = 2 };  // weight rule of a frame
 // FRAME_SLIM (trace_sample's frames): the rule is rebuilt from the material, omtr from tr (trans_split
 // forms omtr as 1 - tr on every path), the node id from the returning child's id and the generation
-// from the stack index, so a Fresnel frame writes 24 B fewer to scratch
+// from the stack index, so a Fresnel frame writes 24 B fewer to scratch. C4: writes 143.9 -> 127.0 GB
+// per frame, 456.9 -> 453.8 ms; C5 174.3 -> 173.9 ms; same images (profiles/r05q_frame_slim_ab.log)
 #ifndef RT_FRAME_SLIM
-#define RT_FRAME_SLIM 0
+#define RT_FRAME_SLIM 1
 #endif
 static constexpr bool FRAME_SLIM = RT_FRAME_SLIM != 0;
 template <uint32_t F>
