@@ -116,6 +116,7 @@ struct rt_scene {
     int ntiles;
     int state;       // 0 probe order; 1 a measuring launch was issued; 2 ordered by measured times
     void* measured = nullptr;  // hipEvent_t recorded after the measuring launch, on its stream
+    int tilesX = 0;            // the layout's tiles per row (XCD superblocks)
   };
   std::vector<TileSchedule> schedules;
   struct TileList {  // rt_render_tiles_device / rt_render_pixels_device: a validated list and its device copy

@@ -565,6 +565,9 @@ static const Variant& count_variant(const HostScene& h, uint32_t flags) {
 // ray (the probe's tail at N = 8 was 150-340 us of a ~0.9 ms launch). Only the ORDER in
 // which tiles are dispatched depends on it, never a pixel. The probe, the read-back and
 // the sorts run synchronously, once per layout.
+#ifndef RT_XCD_HASH
+#define RT_XCD_HASH 0
+#endif
 static int sort_tiles(rt_scene::TileSchedule& e, hipStream_t st) {
   std::vector<uint32_t> cost(e.ntiles);
   hipError_t r = hipStreamSynchronize(st);
@@ -589,6 +592,32 @@ static int sort_tiles(rt_scene::TileSchedule& e, hipStream_t st) {
   for (int k = NB - 1, acc = 0; k >= 0; --k) { start[k] = acc; acc += hist[k]; }  // longest first
   std::vector<int32_t> order(e.ntiles);
   for (int i = 0; i < e.ntiles; ++i) order[start[key[i]]++] = i;
+#if RT_XCD_HASH > 0
+  // XCD-aware deal (experiment): blocks b and b + 8 share an XCD and its L2 (MI355X_MICROARCH.md).
+  // Superblocks of RT_XCD_HASH x RT_XCD_HASH tiles are hashed to one of 8 lists, each keeping the
+  // longest-first order; dispatch position p takes the next tile of list p % 8, so neighbouring tiles
+  // run on one XCD while every XCD sees the same mix of costs. An empty list's positions take the
+  // longest remaining list's next tile.
+  if (e.tilesX > 0) {
+    constexpr int SB = RT_XCD_HASH;
+    std::vector<int32_t> lists[8];
+    for (int i = 0; i < e.ntiles; ++i) {
+      const int t = order[i], sx = (t % e.tilesX) / SB, sy = (t / e.tilesX) / SB;
+      const uint32_t h = ((uint32_t)sx * 73856093u) ^ ((uint32_t)sy * 19349663u);
+      lists[(h ^ (h >> 7) ^ (h >> 13)) & 7].push_back(t);
+    }
+    size_t pos[8] = {0};
+    for (int p = 0; p < e.ntiles; ++p) {
+      int x = p & 7;
+      if (pos[x] == lists[x].size()) {
+        size_t best = 0;
+        for (int y = 0; y < 8; ++y)
+          if (lists[y].size() - pos[y] > best) { best = lists[y].size() - pos[y]; x = y; }
+      }
+      order[p] = lists[x][pos[x]++];
+    }
+  }
+#endif
   HIPCHK(hipMemcpy(e.order, order.data(), sizeof(int32_t) * e.ntiles, hipMemcpyHostToDevice));
   return RT_OK;
 }
@@ -616,6 +645,7 @@ static int schedule(rt_scene* s, ParamsD& P, bool count, hipStream_t st) {
                        P, d_cost, ntiles);
     HIPCHK(hipGetLastError());
     s->schedules.push_back({key, d_order, d_cost, ntiles, 0});
+    s->schedules.back().tilesX = tilesX;
     e = &s->schedules.back();
     int rc = sort_tiles(*e, st);
     if (rc) return rc;

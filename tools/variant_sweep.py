@@ -121,6 +121,10 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "h8s13": ["RT_KNN_H8=1", "RT_KNN_START=1.3"],
     "slim0": ["RT_FRAME_SLIM=0"],             # shading-tree frames with every field (round 4)
     "slim1": ["RT_FRAME_SLIM=1"],             # ... without the fields derivable at the fold
+    "xh0": ["RT_XCD_HASH=0"],                 # longest-first tile order, blocks dealt to XCDs as they come
+    "xh2": ["RT_XCD_HASH=2"],                 # 2x2-tile superblocks hashed to one XCD's list
+    "xh4": ["RT_XCD_HASH=4"],
+    "xh8": ["RT_XCD_HASH=8"],
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
