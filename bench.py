@@ -5,18 +5,16 @@ metric  "Mray/s + achieved HBM GB/s, bun69k.cli 1024^2 16spp, 1/2/4/8 GPU"
 workload C3 = scenes/c3_bun69k.cli (data/p3_t09.cli without `wood`) with the
          synthetic bun69k (69,451 triangles), 1024x1024, 16 spp, seed 0x5EED0001.
 
-One step = one full C3 frame: every rank renders its part with the HIP kernel into a device
-buffer -- N > 1: the frame's wave tiles dealt to ranks by their measured wave times
-(multigpu.balanced_tiles; --partition bands: 8-row bands r, r+N, ...) -- then (N>1) the per-rank
-ARGB pixels are gathered to rank 0
-over RCCL (`dist.gather`: one point-to-point send per rank over xGMI) and
-re-interleaved there (the ARGB ints the reference's rndrdImg.pixels holds); frame i's exchange
-overlaps frame i+1's render
-(`multigpu.FrameExchange`, double-buffered tiles) and the last one is drained
-inside the timed region. Work per step is one frame whatever N is
-(strong scaling). value = traced rays of the frame (camera + shadow + reflection
-+ refraction, counted exactly by an instrumented run before timing) / max-over-
-ranks step time.
+One step = one full C3 frame through the native N-GPU group (rt_group_*, csrc/group.hip): every
+rank renders its part of the frame's wave tiles -- a contiguous cut of rank 0's measured wave times,
+re-cut from the ranks' measured render times in setup (rt_group_rebalance), the heaviest tiles
+rendered one sample per wave -- into a device buffer; ranks > 0 pack their ARGB pixels (the ints the
+reference's rndrdImg.pixels holds) and send them to rank 0 over RCCL (grouped ncclSend / ncclRecv,
+each rank's pixels over its own xGMI link), rank 0 scatters them into the frame; frame i's exchange
+overlaps frame i+1's render and the last one is drained inside the timed region (--backend gloo:
+the Python rehearsal of the same step, ranks sharing GPUs). Work per step is one frame whatever N is
+(strong scaling). value = traced rays of the frame (camera + shadow + reflection + refraction,
+counted exactly by an instrumented run before timing) / max-over-ranks step time.
 
 roofline: algorithmic bytes of the render kernel per launch /
 its mean duration from HIP events on the launch stream; peak 8000 GB/s (MI355X HBM3E).
@@ -28,7 +26,8 @@ reported beside it. traffic: measured HBM bytes per launch (FETCH_SIZE x 2 + WRI
 from the newest committed rocprofv3 --pmc summary of the workload in profiles/ when it is of
 this library build (rt_build_id) and its kernel time is within 5 % of this run's, else null
 (traffic_missing says why); fp64: the kernel's fp64 FLOP rate (same PMC summary) against the measured fp64
-VALU peak (tools/fp64_peak.hip).
+VALU peak (tools/fp64_peak.hip); valu: the share of the SIMDs' VALU issue slots the kernel fills (same
+PMC summary) -- the bound this branchy fp64 traversal runs into.
 
 cpu_baseline: the oracle (CPU restatement of the reference path, fp64) timed on
 the box's CPU share (affinity / cgroup quota / OMP_NUM_THREADS; the host's CPU count and model
@@ -50,6 +49,7 @@ sys.path.insert(0, str(REPO))
 METRIC = "Mray/s + achieved HBM GB/s, bun69k.cli 1024² 16spp, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_COPY_PEAK_GBPS = 6300.0  # measured float4-copy peak (MI355X_MICROARCH.md)
+SIMD_CLOCK_HZ = 2.4e9  # MI355X max engine clock (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 74.07  # measured: tools/fp64_peak.hip on MI355X (profiles/r02_fp64_peak.json)
 
 # Algorithmic bytes per counted event: SURVEY.md 8(d)'s per-ray formula, records at the
@@ -409,7 +409,7 @@ def main():
         bid = rt.build_id()
         pmc, tsrc, why = find_pmc(workload, bid, kern_ms) if world == 1 else (None, None, "N > 1")
         traffic = traffic_rd = traffic_wr = traffic_lo = None
-        fp64 = None
+        fp64 = valu = None
         if pmc:
             traffic_rd = float(pmc["hbm_bytes_per_launch"])
             traffic_wr = pmc.get("hbm_write_bytes_per_launch")
@@ -420,6 +420,21 @@ def main():
                 fp64 = {"tflops": tf, "peak_tflops_measured": FP64_PEAK_TFLOPS, "frac": tf / FP64_PEAK_TFLOPS,
                         "flop_per_launch": float(pmc["fp64_flop_per_launch"]),
                         "note": "fp64 VALU wave instructions x 64 lanes (inactive lanes included: an upper bound)"}
+            cnt = pmc.get("counters") or {}
+            if cnt.get("SQ_INSTS_VALU"):
+                # the bound this fp64 traversal actually runs into: the SIMDs' VALU issue. A wave64 VALU
+                # instruction occupies a 16-lane SIMD for 4 cycles (the fp64 FMA rate the peak is quoted on)
+                n_simd = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+                cyc = n_simd * SIMD_CLOCK_HZ * (kern_ms / 1e3)
+                valu = {"issue_frac": float(cnt["SQ_INSTS_VALU"]) * 4 / cyc,
+                        "active_frac": float(cnt.get("SQ_ACTIVE_INST_VALU", 0)) * 4 / cyc,
+                        "resident_waves_per_simd": float(cnt.get("SQ_WAVE_CYCLES", 0)) * 4 / cyc,
+                        "wave_instructions_per_launch": float(cnt["SQ_INSTS_VALU"]),
+                        "salu_instructions_per_launch": float(cnt.get("SQ_INSTS_SALU", 0)),
+                        "simds": n_simd, "clock_ghz": SIMD_CLOCK_HZ / 1e9,
+                        "note": "SQ_INSTS_VALU x 4 cycles / (SIMDs x max clock x kernel time): the share of the "
+                                "SIMDs' VALU issue slots the kernel fills (SQ_ACTIVE_INST_VALU and SQ_WAVE_CYCLES "
+                                "count in 4-cycle units); from the same build's PMC summary"}
         out = {
             "metric": METRIC,
             "value": rays_frame / (ms_per_step / 1e3) / 1e6,
@@ -478,7 +493,7 @@ def main():
                          # ... and the same per-lane accounting of the work the kernel does (culling on)
                          "cache_served_gbps_8d_per_lane_executed": achieved_lane_x,
                          "bytes_per_ray_8d_per_lane_executed": xbytes_frame / max(1.0, rays_frame),
-                         "fp64": fp64},
+                         "fp64": fp64, "valu": valu},
         }
         if world > 1 and args.backend == "gloo":
             out["rehearsal"] = f"gloo backend, {world} ranks on {ndev} GPU(s): not a scaling measurement"
