@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--rebalance", type=int, default=0, help="rt_group_rebalance rounds before timing")
+    ap.add_argument("--heavy", type=float, default=0.0, help="plan: split tiles above heavy x a slot's share (0: 1.25)")
+    ap.add_argument("--slots", type=int, default=0, help="plan: wave slots per rank (0: 4096)")
     ap.add_argument("--out")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime: torch's)
@@ -37,7 +39,7 @@ def main():
         g.build_photons(seed)
     full = g.time_render(W, H, spp=spp, seed=seed, warmup=2, iters=5)
     rows = []
-    with rt.Group.create([g] * a.world, W, H, spp=spp, seed=seed, copy=True) as grp:
+    with rt.Group.create([g] * a.world, W, H, spp=spp, seed=seed, copy=True, heavy=a.heavy, slots=a.slots) as grp:
         if a.rebalance:
             ms = grp.rebalance(rounds=a.rebalance, iters=10)
             print(json.dumps({"rebalanced_rank_ms": ms.tolist()}), flush=True)
@@ -51,7 +53,7 @@ def main():
     smax = max(x["step_ms"] for x in rows)
     kmax = max(x["kernel_ms"] for x in rows)
     out = {"config": a.config, "workload": f"{cli} {W}x{H} {spp}spp", "world": a.world, "iters": a.iters,
-           "rebalance_rounds": a.rebalance,
+           "rebalance_rounds": a.rebalance, "heavy": a.heavy or 1.25, "slots": a.slots or 4096,
            "full_frame_kernel_ms": full, "max_step_ms": smax, "max_kernel_ms": kmax,
            "step_minus_kernel_us": (smax - kmax) * 1e3,
            "emulated_efficiency": full / a.world / smax, "kernel_efficiency": full / a.world / kmax,

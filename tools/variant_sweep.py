@@ -125,6 +125,8 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "xh2": ["RT_XCD_HASH=2"],                 # 2x2-tile superblocks hashed to one XCD's list
     "xh4": ["RT_XCD_HASH=4"],
     "xh8": ["RT_XCD_HASH=8"],
+    "sc0": ["RT_SLAB_CALL=0"],                # exact slab fallback inlined in the traversal loops
+    "sc1": ["RT_SLAB_CALL=1"],                # ... as a real call
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
