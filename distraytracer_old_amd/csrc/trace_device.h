@@ -206,23 +206,58 @@ DEVI int slab_apx(const double* mn, const double* mx, V o, const double* y, doub
   if (-diff > tol) return 0;
   return -1;
 }
+// The same approximate test as two masks instead of a tri-state int (RT_APX2): `sure` -- the box
+// decision is settled (a miss, or a hit / miss beyond the margin); the return value -- a settled hit.
+// The compares feed the branch as lane masks; the int's selects and re-compares are gone.
+#ifndef RT_APX2
+#define RT_APX2 0
+#endif
+DEVI bool slab_apx2(const double* mn, const double* mx, V o, const double* y, double& lo, bool& sure) {
+  const double b0 = mn[0], b1 = mn[1], b2 = mn[2], b3 = mx[0], b4 = mx[1], b5 = mx[2];
+  const double t0 = (b0 - o.x) * y[0], t3 = (b3 - o.x) * y[0];
+  const double t1 = (b1 - o.y) * y[1], t4 = (b4 - o.y) * y[1];
+  const double t2 = (b2 - o.z) * y[2], t5 = (b5 - o.z) * y[2];
+  lo = fmax(fmax(fmin(t0, t3), fmin(t1, t4)), fmin(t2, t5));
+  const double hi = fmin(fmin(fmax(t0, t3), fmax(t1, t4)), fmax(t2, t5));
+  const bool pos = lo > 0;
+  const double diff = hi - lo, tol = APX * (fabs(hi) + fabs(lo));
+  const bool in = diff > tol;
+  sure = !pos || in || (-diff > tol);
+  return pos && in;
+}
 DEVI bool slab_exact(const double* mn, const double* mx, V o, V d, const RayInv& ri, double& tEntry) {
   if (ri.fast) return slab_t<true>(mn, mx, o, d, ri.y, tEntry);
   return slab_t<false>(mn, mx, o, d, nullptr, tEntry);
 }
 // hit?  (myBBox.intersectCheck != null)
+template <bool A2 = (RT_APX2 != 0)>  // A2: slab_apx2 (lane masks)
 DEVI bool box_hit(const double* mn, const double* mx, V o, V d, const RayInv& ri) {
   double te;
-  if (ri.fast) {
+  if (A2 && ri.fast) {
+    bool sure;
+    const bool h = slab_apx2(mn, mx, o, ri.y, te, sure);
+    if (sure) return h;
+  } else if (ri.fast) {
     int r = slab_apx(mn, mx, o, ri.y, te);
     if (r >= 0) return r != 0;
   }
   return slab_exact(mn, mx, o, d, ri, te);
 }
 // hit and (lim == DMAX or entry t < lim)   (BVH right-child rule)
+template <bool A2 = (RT_APX2 != 0)>  // A2: slab_apx2 (lane masks)
 DEVI bool box_before(const double* mn, const double* mx, V o, V d, const RayInv& ri, double lim) {
   double te;
-  if (ri.fast) {
+  if (A2 && ri.fast) {
+    bool sure;
+    const bool h = slab_apx2(mn, mx, o, ri.y, te, sure);
+    if (sure) {
+      if (!h) return false;
+      if (lim == DMAX) return true;
+      const double tol = APX * (fabs(te) + fabs(lim));
+      if (lim - te > tol) return true;
+      if (te - lim > tol) return false;
+    }
+  } else if (ri.fast) {
     int r = slab_apx(mn, mx, o, ri.y, te);
     if (r == 0) return false;
     if (r == 1) {
@@ -236,9 +271,19 @@ DEVI bool box_before(const double* mn, const double* mx, V o, V d, const RayInv&
   return lim == DMAX || te < lim;
 }
 // hit and dist - entry t > 1e-7   (calcShadowHit on a box)
+template <bool A2 = (RT_APX2 != 0)>  // A2: slab_apx2 (lane masks)
 DEVI bool box_shadow(const double* mn, const double* mx, V o, V d, const RayInv& ri, double dist) {
   double te;
-  if (ri.fast) {
+  if (A2 && ri.fast) {
+    bool sure;
+    const bool h = slab_apx2(mn, mx, o, ri.y, te, sure);
+    if (sure) {
+      if (!h) return false;
+      const double g = (dist - te) - EPS, tol = APX * (fabs(te) + fabs(dist));
+      if (g > tol) return true;
+      if (-g > tol) return false;
+    }
+  } else if (ri.fast) {
     int r = slab_apx(mn, mx, o, ri.y, te);
     if (r == 0) return false;
     if (r == 1) {
@@ -252,8 +297,18 @@ DEVI bool box_shadow(const double* mn, const double* mx, V o, V d, const RayInv&
 
 // box_shadow that also reports the box's entry t (approximate: the ordering of the nearest-first
 // any-hit traversal, never a decision)
+template <bool A2 = (RT_APX2 != 0)>  // A2: slab_apx2 (lane masks)
 DEVI bool box_shadow_e(const double* mn, const double* mx, V o, V d, const RayInv& ri, double dist, double& te) {
-  if (ri.fast) {
+  if (A2 && ri.fast) {
+    bool sure;
+    const bool h = slab_apx2(mn, mx, o, ri.y, te, sure);
+    if (sure) {
+      if (!h) return false;
+      const double g = (dist - te) - EPS, tol = APX * (fabs(te) + fabs(dist));
+      if (g > tol) return true;
+      if (-g > tol) return false;
+    }
+  } else if (ri.fast) {
     int r = slab_apx(mn, mx, o, ri.y, te);
     if (r == 0) return false;
     if (r == 1) {

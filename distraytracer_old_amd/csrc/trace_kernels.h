@@ -156,7 +156,26 @@ DEVI int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 DEVI uint64_t uni64(uint64_t v) {
   return ((uint64_t)(uint32_t)uni((int32_t)(v >> 32)) << 32) | (uint32_t)uni((int32_t)(uint32_t)v);
 }
-DEVI bool in_mask(uint64_t m) { return (m >> __lane_id()) & 1; }
+// this lane's bit of a wave-uniform lane mask. RT_INV_BALLOT: as the mask itself (inverse ballot: the
+// SGPR mask becomes the branch's exec / vcc mask, no per-lane shift and compare on the VALU)
+#ifndef RT_INV_BALLOT
+#define RT_INV_BALLOT 0
+#endif
+template <bool IB = (RT_INV_BALLOT != 0)>
+DEVI bool in_mask_t(uint64_t m) {
+  if constexpr (IB) return __builtin_amdgcn_inverse_ballot_w64(m);
+  else return (m >> __lane_id()) & 1;
+}
+DEVI bool in_mask(uint64_t m) { return in_mask_t<>(m); }
+// MASKOPS<F>: the packet traversals' lane bits by inverse ballot and their approximate box tests as
+// lane masks (slab_apx2) -- C3 3.024 -> 2.994 ms, but C4's transparent variant 453 -> 459 ms through
+// its allocation, C5 unchanged (profiles/r05w_maskops_ab.log): on in the variants without
+// transparent materials (RT_MASKOPS 1), everywhere (2) or nowhere (0)
+#ifndef RT_MASKOPS
+#define RT_MASKOPS 1
+#endif
+template <uint32_t F>
+static constexpr bool MASKOPS = RT_MASKOPS == 2 || (RT_MASKOPS == 1 && (F & FT_TRANS) == 0);
 #ifdef RT_PROF_PKSTAT
 __device__ unsigned long long rt_pk_stat[12];
 // one wave step testing the lanes in m: counted once per wave (by its first active lane)
@@ -390,7 +409,7 @@ DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, RayInv ri,
       st.setN(sp, N << 1);
       sp++;
       local = DMAX;
-      if (box_hit(nd.lmin, nd.lmax, ao, ad, ri)) N = nd.left;
+      if (box_hit<MASKOPS<F>>(nd.lmin, nd.lmax, ao, ad, ri)) N = nd.left;
       else { N = INT32_MAX; break; }
     }
     if (N != INT32_MAX) {
@@ -403,7 +422,7 @@ DEVI void accel_closest(const SceneD& S, const AccelD& A, V ao, V ad, RayInv ri,
       const int32_t np = st.getN(sp - 1);
       if ((np & 1) == 0) {
         const NodeD& nd = S.node[np >> 1];
-        if (box_before(nd.rmin, nd.rmax, ao, ad, ri, local)) {
+        if (box_before<MASKOPS<F>>(nd.rmin, nd.rmax, ao, ad, ri, local)) {
           st.setN(sp - 1, np | 1);
           N = nd.right;
           break;
@@ -496,18 +515,18 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
       PKSTAT(P_CB_STEP, act);
       WCNT(C_WNODE, 1);  // the node's record: left half now, right half at the unwind
       bool hl = false;
-      if (in_mask(act)) {
+      if (in_mask_t<MASKOPS<F>>(act)) {
         if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }
         st.setT(sp, local);
         local = DMAX;
-        hl = box_hit(cl.mn, cl.mx, ao, ad, ri);
+        hl = box_hit<MASKOPS<F>>(cl.mn, cl.mx, ao, ad, ri);
       }
       sp++;
       const uint64_t H = __ballot(hl);
       if (H) { act = H; N = cl.ref; }
       else { N = INT32_MAX; break; }
     }
-    if (N != INT32_MAX && in_mask(act)) leaf_closest<CNT, F, false, true>(S, ~N, axf, ao, ad, w, k, hc, best, local, ct);
+    if (N != INT32_MAX && in_mask_t<MASKOPS<F>>(act)) leaf_closest<CNT, F, false, true>(S, ~N, axf, ao, ad, w, k, hc, best, local, ct);
     // unwind
     N = INT32_MAX;
     while (sp > 0) {
@@ -517,7 +536,7 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
         const ChildBox cr = sload_child(S.node + (np >> 1), 1);
         PKSTAT(P_CB_STEP, M);
         bool gr = false;
-        if (in_mask(M)) gr = box_before(cr.mn, cr.mx, ao, ad, ri, local);
+        if (in_mask_t<MASKOPS<F>>(M)) gr = box_before<MASKOPS<F>>(cr.mn, cr.mx, ao, ad, ri, local);
         const uint64_t R = __ballot(gr);
         if (R) {
           st.setN(sp - 1, np | 1);
@@ -527,7 +546,7 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
         }
       }
       // this node's minimal t joins the enclosing subtree's
-      if (in_mask(M)) {
+      if (in_mask_t<MASKOPS<F>>(M)) {
         const double sv = st.getT(sp - 1);
         if (sv < local) local = sv;
       }
@@ -618,13 +637,13 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
       WCNT(C_WNODE, 1);  // a node visit (8(d) prices one at 64 B, as the reference order's)
       bool hl = false, hr = false;
       double el = DMAX, er = DMAX;
-      if (in_mask(act)) {
+      if (in_mask_t<MASKOPS<F>>(act)) {
         if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }
         const double bnd = fmin(best.t, bt), lim = fmin(bnd + bnd * 0x1p-40, 0x1p1000);  // a miss (DMAX) never passes
         el = entry_grown(cl.mn, cl.mx, sl, ao, ri.y);
         er = entry_grown(cr.mn, cr.mx, sr, ao, ri.y);
-        if (el <= lim) hl = box_hit(cl.mn, cl.mx, ao, ad, ri);
-        if (er <= lim) hr = box_hit(cr.mn, cr.mx, ao, ad, ri);
+        if (el <= lim) hl = box_hit<MASKOPS<F>>(cl.mn, cl.mx, ao, ad, ri);
+        if (er <= lim) hr = box_hit<MASKOPS<F>>(cr.mn, cr.mx, ao, ad, ri);
       }
       const uint64_t L = __ballot(hl), R = __ballot(hr);
       if (L && R) {
@@ -633,7 +652,7 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
         const uint64_t far = nearLeft ? R : L;
         pkN()[sp] = (N << 1) | (nearLeft ? 1 : 0);
         pkM()[sp] = far;
-        if (sp < PK_LDS && in_mask(far)) pkT()[sp * 64 + __lane_id()] = nearLeft ? er : el;
+        if (sp < PK_LDS && in_mask_t<MASKOPS<F>>(far)) pkT()[sp * 64 + __lane_id()] = nearLeft ? er : el;
         sp++;
 #if RT_NF_CODE
         curCode = (N << 1) | (nearLeft ? 0 : 1);
@@ -662,12 +681,12 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
     } else {  // a leaf: a run of triangles in leaf order
       const int32_t c = ~N;
       const int32_t st = (c >> 5) & LEAF_RUN_MAXSTART, cnt = c & 31;
-      if (CNT && in_mask(act)) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += cnt; }
+      if (CNT && in_mask_t<MASKOPS<F>>(act)) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += cnt; }
       for (int i = 0; i < cnt; ++i) {
         PKSTAT(P_CT_STEP, act);
         WCNT(C_WTRI, 1);
         const TriG T = sload_tri(S.tri + st + i);
-        if (in_mask(act)) {
+        if (in_mask_t<MASKOPS<F>>(act)) {
           if (CNT) ct.c[C_TRI]++;
           double t;
           int args;
@@ -692,7 +711,7 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
       uint64_t M = uni64(pkM()[sp]);
       const ChildBox cb = sload_child(S.node + (code >> 1), code & 1);
       bool keep = false;
-      if (in_mask(M)) {
+      if (in_mask_t<MASKOPS<F>>(M)) {
         const double bnd = fmin(best.t, bt), lim = fmin(bnd + bnd * 0x1p-40, 0x1p1000);  // a miss (DMAX) never passes
         const double e = sp < PK_LDS ? pkT()[sp * 64 + __lane_id()]
                                      : entry_grown(cb.mn, cb.mx, sload_slack(S.node + (code >> 1), code & 1), ao, ri.y);
@@ -738,7 +757,7 @@ DEVI void inst_closest(const SceneD& S, int32_t ii, WRay& w, const Key& k, int t
       const AccelD& A = S.accel[I.pad[0]];
       if (CNT) { ct.c[C_ROOT]++; ct.c[C_BOX]++; }
       const RayInv ri = ray_inv(wi.o, wi.d, S.fastSlab & SCENE_FAST_SLAB);
-      if (!box_hit(A.bmin, A.bmax, wi.o, wi.d, ri)) return;  // myAccelStruct.intersectCheck root box
+      if (!box_hit<MASKOPS<F>>(A.bmin, A.bmax, wi.o, wi.d, ri)) return;  // myAccelStruct.intersectCheck root box
       accel_closest<CNT, F, true>(S, A, wi.o, wi.d, ri, wi, k, hc, best, local, ct);
     } else {
       double t;
@@ -936,7 +955,7 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
       const AccelD A = PK ? sload_accel(S.accel + tp.idx) : S.accel[tp.idx];
       if (CNT) { ct.c[C_ROOT]++; ct.c[C_BOX]++; }
       RayInv ri = ray_inv(o, d, S.fastSlab & SCENE_FAST_SLAB);
-      if (!box_hit(A.bmin, A.bmax, o, d, ri)) continue;
+      if (!box_hit<MASKOPS<F>>(A.bmin, A.bmax, o, d, ri)) continue;
       w.moved = false;
       double local = DMAX;
       PROF_T0(t_acc);
@@ -964,10 +983,10 @@ DEVI Best closest(const SceneD& S, WRay& w, const Key& k, Counters& ct) {
 
 // any-hit: mySceneObject/myBBox/myGeomList/myBVH.calcShadowHit (mySceneObject.java:33-38,
 // myGeomBase.java:166-170, 268-277, 397-404): blocked iff hit && dist - t > 1e-7
-template <bool CNT>
+template <bool CNT, bool A2 = (RT_APX2 != 0)>
 DEVI bool shadow_box(const double* mn, const double* mx, V o, V d, const RayInv& ri, double dist, Counters& ct) {
   if (CNT) ct.c[C_BOX]++;
-  return box_shadow(mn, mx, o, d, ri, dist);
+  return box_shadow<A2>(mn, mx, o, d, ri, dist);
 }
 template <bool CNT, uint32_t F>
 DEVI bool inst_any(const SceneD& S, int32_t ii, const WRay& w, const Key& k, double dist, Counters& ct);
@@ -1055,7 +1074,7 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
   // leafVals.calcShadowHit tests its own box first; myBVH.calcShadowHit (internal) does not
   if (N < 0) {
     bool hb = false;
-    if (in_mask(act)) hb = shadow_box<CNT>(A.bmin, A.bmax, ao, ad, ri, dist, ct);
+    if (in_mask_t<MASKOPS<F>>(act)) hb = shadow_box<CNT, MASKOPS<F>>(A.bmin, A.bmax, ao, ad, ri, dist, ct);
     act = __ballot(hb);
     if (!act) return false;
   }
@@ -1067,10 +1086,10 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
       WCNT(C_WNODE, 1);
       bool hl = false, hr = false;
       double el = DMAX, er = DMAX;
-      if (in_mask(act)) {
+      if (in_mask_t<MASKOPS<F>>(act)) {
         if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX]++; }
-        hl = box_shadow_e(cl.mn, cl.mx, ao, ad, ri, dist, el);
-        hr = box_shadow_e(cr.mn, cr.mx, ao, ad, ri, dist, er);
+        hl = box_shadow_e<MASKOPS<F>>(cl.mn, cl.mx, ao, ad, ri, dist, el);
+        hr = box_shadow_e<MASKOPS<F>>(cr.mn, cr.mx, ao, ad, ri, dist, er);
       }
       const uint64_t R = __ballot(hr);
       const uint64_t H = __ballot(hl);
@@ -1086,7 +1105,7 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
       if (H) { act = H; N = cl.ref; continue; }
     } else if (N != INT32_MAX) {
       bool b = false;
-      if (in_mask(act)) b = leaf_any<CNT, F, false, true>(S, ~N, axf, ao, ad, w, k, dist, ct);
+      if (in_mask_t<MASKOPS<F>>(act)) b = leaf_any<CNT, F, false, true>(S, ~N, axf, ao, ad, w, k, dist, ct);
       if (b) blocked = true;
       alive &= ~__ballot(b);
       if (!alive) return blocked;
@@ -1094,7 +1113,7 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
     N = INT32_MAX;
     while (sp > 0) {
       --sp;
-      if (CNT && in_mask(st.getM(sp) & alive)) ct.c[C_BOX]++;
+      if (CNT && in_mask_t<MASKOPS<F>>(st.getM(sp) & alive)) ct.c[C_BOX]++;
       const uint64_t R = st.getR(sp) & alive;
       if (R) { act = R; N = st.getC(sp); break; }
     }

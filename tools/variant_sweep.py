@@ -127,6 +127,13 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "xh8": ["RT_XCD_HASH=8"],
     "sc0": ["RT_SLAB_CALL=0"],                # exact slab fallback inlined in the traversal loops
     "sc1": ["RT_SLAB_CALL=1"],                # ... as a real call
+    "apx0": ["RT_APX2=0"],                    # approximate box test returning a tri-state int
+    "apx1": ["RT_APX2=1"],                    # ... as two lane masks (settled, hit)
+    "ib0": ["RT_INV_BALLOT=0"],               # a lane's bit of a wave mask by shift and compare
+    "ib1": ["RT_INV_BALLOT=1"],               # ... by inverse ballot (the mask as exec)
+    "ib1apx1": ["RT_INV_BALLOT=1", "RT_APX2=1"],
+    "mo0": ["RT_MASKOPS=0"],                  # packet lane bits by shift, tri-state approximate box tests
+    "mo1": ["RT_MASKOPS=1"],                  # inverse ballot + lane-mask box tests in opaque variants (default)
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
