@@ -134,6 +134,10 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "ib1apx1": ["RT_INV_BALLOT=1", "RT_APX2=1"],
     "mo0": ["RT_MASKOPS=0"],                  # packet lane bits by shift, tri-state approximate box tests
     "mo1": ["RT_MASKOPS=1"],                  # inverse ballot + lane-mask box tests in opaque variants (default)
+    "tl0": [],                                # (the default build)
+    "tlsum": ["RT_SUMS_LDS_TRANS=1"],         # per-pixel sums in LDS in the transparent variants
+    "tlres": ["RT_RES_LDS_TRANS=1"],          # finished colours in LDS in the transparent variants
+    "tlboth": ["RT_SUMS_LDS_TRANS=1", "RT_RES_LDS_TRANS=1"],
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
