@@ -2719,14 +2719,25 @@ static constexpr int MAX_FRAMES = 7;  // gen < numRays-2 = 6 -> at most 6 nodes 
 // traversal levels, stash slots), except the per-lane stacks of the photon scans and of the
 // lane-wise BVH experiment (RT_LANE_DIV), which index [level][lane] ints over the same bytes -- so
 // not in photon variants nor with RT_LANE_DIV. Measured (profiles/r04z_res_lds_ab.txt): C3 writes
-// 1.36 -> 1.31 GB per frame at the same time; C4's transparent variant lost 1.8 % (its allocation
-// shifts), so it keeps its VGPRs.
+// 1.36 -> 1.31 GB per frame at the same time; C4's transparent variant lost 1.8 % then (its allocation
+// shifted) and gains since round 5 (below).
+// Round 5, after the scalar primitive loads and slim frames shifted C4's allocation: the per-pixel
+// sums and the finished colour in LDS pay in the transparent variants without a photon map too --
+// C4 455.3 -> 447.4 ms, writes 127.0 -> 113.1 GB per frame; C5's photon variant keeps its sums in
+// VGPRs (177.6 vs 174.4 ms with them in LDS), same images (profiles/r05z_trans_lds_ab.log)
+#ifndef RT_RES_LDS_TRANS
+#define RT_RES_LDS_TRANS 1
+#endif
+#ifndef RT_SUMS_LDS_TRANS
+#define RT_SUMS_LDS_TRANS 1
+#endif
 #ifndef RT_RES_LDS
 #define RT_RES_LDS 1
 #endif
 enum { SL_RES = SL_RGB };
 template <uint32_t F>
-static constexpr bool RES_LDS = RT_RES_LDS != 0 && STASH_SHADE && (F & (FT_PHOTON | FT_TRANS)) == 0 && RT_LANE_DIV == 0;
+static constexpr bool RES_LDS = RT_RES_LDS != 0 && STASH_SHADE && (F & FT_PHOTON) == 0 &&
+                                ((F & FT_TRANS) == 0 || RT_RES_LDS_TRANS != 0) && RT_LANE_DIV == 0;
 
 // reflectRay (myScene.java:907-914) for the whole shading tree of one camera sample
 template <bool CNT, uint32_t F>
@@ -3364,7 +3375,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
   // in registers (rs / gs / bs; the 1-spp non-DOF path keeps its one colour there). Which is
   // faster depends on the variant's register allocation (measured: C3's F = 0 gains, C4's
   // transparent variant loses 6 %).
-  constexpr bool SUMS_LDS = (F & FT_TRANS) == 0;
+  constexpr bool SUMS_LDS = (F & FT_TRANS) == 0 || (RT_SUMS_LDS_TRANS != 0 && (F & FT_PHOTON) == 0);
   double rs = 0, gs = 0, bs = 0;
   lds_f64* sums = (lds_f64*)((lds_u8*)rt_lds + LDS_BYTES);
   if (SUMS_LDS && G > 1 && (lane & (G - 1)) == 0) {
