@@ -138,6 +138,9 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "tlsum": ["RT_SUMS_LDS_TRANS=1"],         # per-pixel sums in LDS in the transparent variants
     "tlres": ["RT_RES_LDS_TRANS=1"],          # finished colours in LDS in the transparent variants
     "tlboth": ["RT_SUMS_LDS_TRANS=1", "RT_RES_LDS_TRANS=1"],
+    "fin": [],                                # the final build's settings (A of the last A/Bs)
+    "mo2": ["RT_MASKOPS=2"],                  # mask ops in every variant
+    "mo2xh4": ["RT_MASKOPS=2", "RT_XCD_HASH=4"],
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
