@@ -609,6 +609,37 @@ DEVI double entry_grown(const double* mn, const double* mx, double s, V o, const
   const double hi = fmin(fmin(fmax(t0, t3), fmax(t1, t4)), fmax(t2, t5));
   return (hi >= lo && hi > 0) ? lo : DMAX;
 }
+// RT_NF_LB: a child's grown-box entry from its exact box's own slab values -- every axis's entry moves
+// by at most s |y_axis| when the box grows by s, so lo - s max|y| is a lower bound of the grown entry
+// within s max|y| of it: pruning by it is conservative (it prunes no subtree the exact grown entry
+// keeps), ordering by it changes no answer (nearest-first finds h* in any order), and the box's hit
+// decision reuses the same six slab values instead of a second slab computation. C3 2.995 -> 2.926 ms,
+// same image (profiles/r05zc_c3_nf_lb_ab.log)
+#ifndef RT_NF_LB
+#define RT_NF_LB 1
+#endif
+template <bool A2>
+DEVI bool nf_child(const ChildBox& c, double s, double ymax, V o, V d, const RayInv& ri, double lim, double& e) {
+  if (!ri.fast) {
+    e = entry_grown(c.mn, c.mx, s, o, ri.y);
+    return e <= lim && box_hit<A2>(c.mn, c.mx, o, d, ri);
+  }
+  double lo;
+  bool sure;
+  const bool h = slab_apx2(c.mn, c.mx, o, ri.y, lo, sure);
+  e = DMAX;
+  if (sure) {  // a settled hit has a finite entry lo > 0
+    if (!h) return false;
+    const double lb = lo - s * ymax;  // ymax = inf (an axis-parallel ray): -inf, never pruned
+    if (!(lb <= lim)) return false;
+    e = lb;
+    return true;
+  }
+  double te;  // unsettled (grazing): the exact test, and the grown entry by its own computation
+  if (!slab_exact(c.mn, c.mx, o, d, ri, te)) return false;
+  e = entry_grown(c.mn, c.mx, s, o, ri.y);
+  return e <= lim;
+}
 // a candidate t worth the inside test: it can beat (or, by leaf order, tie) this accel's best
 // and beats the best of the entries before it (their ties win: TreeMap keeps the first)
 struct LimNF {
@@ -624,6 +655,7 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
   uint64_t act = __ballot(1);
   int sp = 0;
   int32_t N = uni(A.root);
+  const double ymax = fmax(fmax(fabs(ri.y[0]), fabs(ri.y[1])), fabs(ri.y[2]));  // RT_NF_LB
 #if RT_NF_CODE
   int32_t curCode = 0;    // the child being entered (node << 1 | side): its box is reloaded for the inside test
 #else
@@ -640,10 +672,15 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
       if (in_mask_t<MASKOPS<F>>(act)) {
         if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }
         const double bnd = fmin(best.t, bt), lim = fmin(bnd + bnd * 0x1p-40, 0x1p1000);  // a miss (DMAX) never passes
-        el = entry_grown(cl.mn, cl.mx, sl, ao, ri.y);
-        er = entry_grown(cr.mn, cr.mx, sr, ao, ri.y);
-        if (el <= lim) hl = box_hit<MASKOPS<F>>(cl.mn, cl.mx, ao, ad, ri);
-        if (er <= lim) hr = box_hit<MASKOPS<F>>(cr.mn, cr.mx, ao, ad, ri);
+        if constexpr (RT_NF_LB != 0) {
+          hl = nf_child<MASKOPS<F>>(cl, sl, ymax, ao, ad, ri, lim, el);
+          hr = nf_child<MASKOPS<F>>(cr, sr, ymax, ao, ad, ri, lim, er);
+        } else {
+          el = entry_grown(cl.mn, cl.mx, sl, ao, ri.y);
+          er = entry_grown(cr.mn, cr.mx, sr, ao, ri.y);
+          if (el <= lim) hl = box_hit<MASKOPS<F>>(cl.mn, cl.mx, ao, ad, ri);
+          if (er <= lim) hr = box_hit<MASKOPS<F>>(cr.mn, cr.mx, ao, ad, ri);
+        }
       }
       const uint64_t L = __ballot(hl), R = __ballot(hr);
       if (L && R) {

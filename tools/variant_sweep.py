@@ -141,6 +141,8 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "fin": [],                                # the final build's settings (A of the last A/Bs)
     "mo2": ["RT_MASKOPS=2"],                  # mask ops in every variant
     "mo2xh4": ["RT_MASKOPS=2", "RT_XCD_HASH=4"],
+    "lb0": ["RT_NF_LB=0"],                    # nearest-first: grown-box entry by its own slab computation
+    "lb1": ["RT_NF_LB=1"],                    # ... as a lower bound from the exact box's slab values
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
