@@ -143,6 +143,7 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "mo2xh4": ["RT_MASKOPS=2", "RT_XCD_HASH=4"],
     "lb0": ["RT_NF_LB=0"],                    # nearest-first: grown-box entry by its own slab computation
     "lb1": ["RT_NF_LB=1"],                    # ... as a lower bound from the exact box's slab values
+    "kd0": ["RT_KNN_DIV=0"],                  # kNN scans as packets only
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
