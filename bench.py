@@ -12,7 +12,9 @@ rendered one sample per wave -- into a device buffer; ranks > 0 pack their ARGB 
 reference's rndrdImg.pixels holds) and send them to rank 0 over RCCL (grouped ncclSend / ncclRecv,
 each rank's pixels over its own xGMI link), rank 0 scatters them into the frame; frame i's exchange
 overlaps frame i+1's render and the last one is drained inside the timed region (--backend gloo:
-the Python rehearsal of the same step, ranks sharing GPUs). Work per step is one frame whatever N is
+the same native rank mode over the host transport, ranks sharing GPUs -- a rehearsal, not a scaling
+measurement). After timing, rank 0 checks the assembled frame against rt_render bit for bit
+(frame_check). Work per step is one frame whatever N is
 (strong scaling). value = traced rays of the frame (camera + shadow + reflection + refraction,
 counted exactly by an instrumented run before timing) / max-over-ranks step time.
 
@@ -223,7 +225,11 @@ def main():
     ap.add_argument("--partition", default="tiles", choices=["tiles", "bands"],
                     help="N > 1: cost-balanced wave tiles (default) or interleaved 8-row bands")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo: rehearse the N-rank step on fewer GPUs (tiles staged to host; ranks share devices)")
+                    help="gloo: rehearse the N-rank step on fewer GPUs (the native group over the host transport "
+                         "on gloo, pixels staged through host memory; ranks share devices)")
+    ap.add_argument("--impl", default="native", choices=["native", "python"],
+                    help="N > 1: the native group (rt_group_create_comm, default) or the Python rank path "
+                         "(multigpu.RankRenderer over torch.distributed)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -268,29 +274,39 @@ def main():
     scene = rt.Scene.load_cli(cli, textures=tex, device=dev)
     scene_load_s = time.perf_counter() - t
     info = scene.info()
-    photon_s = None
-    if info["photon_mode"]:  # photon pre-pass (initRender), outside the timed region; sharded over ranks
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        multigpu.build_photons_sharded(scene, seed, info["photon_count"], dist, device=coll_dev)
-        torch.cuda.synchronize()
-        photon_s = time.perf_counter() - t
-    # the exchanged frame is the reference's output, ARGB ints (rndrdImg.pixels): 4 bytes a pixel.
-    # The N-rank step is the native group (rt_group_*, csrc/group.hip): rank 0 measures the layout's
-    # wave times and broadcasts them, every rank derives the same plan, renders its part, packs it and
-    # sends it to rank 0 over RCCL (ncclSend / ncclRecv), rank 0 scatters it into the frame -- one C
-    # call per frame. N = 1: a one-rank group (every tile, no exchange). --backend gloo (ranks
-    # sharing one GPU, where RCCL cannot run) rehearses the Python path (multigpu.RankRenderer).
-    native = not (world > 1 and args.backend == "gloo")
-    p_frame = rt.params(W, H, spp=spp, seed=seed)
-    if native:
-        if world > 1:
+    # the ranks' communicator (N > 1, native): RCCL over xGMI, or the host transport on gloo (rehearsals)
+    native = args.impl == "native"
+    comm = None
+    if world > 1 and native:
+        if args.backend == "nccl":
             uid = torch.zeros(128, dtype=torch.uint8, device=coll_dev)
             if rank == 0:
                 uid.copy_(torch.frombuffer(bytearray(rt.group_unique_id()), dtype=torch.uint8))
             dist.broadcast(uid, 0)
-            grp = rt.Group.create_rank(scene, rank, world, bytes(uid.cpu().numpy().tobytes()), W, H, spp=spp,
-                                       seed=seed)
+            comm = rt.Comm.rccl(rank, world, bytes(uid.cpu().numpy().tobytes()), dev)
+        else:
+            comm = rt.Comm.host(dist)
+    photon_s = None
+    if info["photon_mode"]:  # photon pre-pass (initRender), outside the timed region; sharded over ranks
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        if native:  # rt_photons_build_comm: shard, exchange, merge, build -- behind the C ABI
+            scene.build_photons_comm(comm, seed)
+        else:
+            multigpu.build_photons_sharded(scene, seed, info["photon_count"], dist, device=coll_dev)
+        torch.cuda.synchronize()
+        photon_s = time.perf_counter() - t
+    # the exchanged frame is the reference's output, ARGB ints (rndrdImg.pixels): 4 bytes a pixel.
+    # The N-rank step is the native group (rt_group_*, csrc/group.hip): rank 0 measures the layout's
+    # wave times and broadcasts them, every rank derives the same plan (checked collectively), renders
+    # its part, packs it and sends it to rank 0 over RCCL (ncclSend / ncclRecv), rank 0 scatters it
+    # into the frame -- one C call per frame. N = 1: a one-rank group (every tile, no exchange).
+    # --backend gloo (ranks sharing one GPU, where RCCL cannot run): the same native rank mode over
+    # the host transport (pixels staged through host memory); --impl python: multigpu.RankRenderer.
+    p_frame = rt.params(W, H, spp=spp, seed=seed)
+    if native:
+        if world > 1:
+            grp = rt.Group.create_comm(scene, comm, W, H, spp=spp, seed=seed)
         else:
             grp = rt.Group.create([scene], W, H, spp=spp, seed=seed)
         rank_ms_rebalanced = None
@@ -299,8 +315,9 @@ def main():
         run_t, split_t = grp.rank_tiles(rank)
         my_tiles = np.concatenate([run_t, split_t]).astype(np.int32)
         parallelism = ("1 GPU" if world == 1 else
-                       f"cost-balanced wave tiles over {world} ranks (native rt_group, one process per GPU) "
-                       "+ RCCL send/recv of the ARGB pixels to rank 0")
+                       f"cost-balanced wave tiles over {world} ranks (native rt_group, one process per GPU) + "
+                       + ("RCCL send/recv of the ARGB pixels to rank 0" if args.backend == "nccl" else
+                          "host-transport (gloo) send/recv of the ARGB pixels to rank 0"))
 
         def step(ev=None):
             grp.render()
@@ -378,6 +395,19 @@ def main():
         assert nfr == min(args.steps, 64), (nfr, args.steps)
     else:
         kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    # the frame the timed steps produced, checked (after timing): rank 0's assembled ARGB frame against
+    # rt_render of the whole frame on rank 0's GPU, bit for bit (every rank takes part in the frame)
+    frame_check = None
+    if native:
+        _, got = grp.render_host(W, H, rgb=False)
+        if rank == 0:
+            want = np.zeros((H, W), dtype=np.int32)
+            scene.render_argb_into(want, W, H, spp=spp, seed=seed)
+            frame_check = {"bit_exact_vs_rt_render": bool(np.array_equal(got, want)),
+                           "pixels_differing": int((got != want).sum()),
+                           "plan_checks": grp.info()["plan_checks"],
+                           "transport": rt.TRANSPORT_NAMES[grp.info()["rccl"]]}
 
     # the drop-in path's cost (rank 0 of a 1-GPU run): rt_render of the whole frame into a host ARGB
     # buffer -- what the JNI draw() does: launch + the 4 B/pixel read-back to
@@ -457,6 +487,7 @@ def main():
             "camera_msamples_per_s": cam_frame / (ms_per_step / 1e3) / 1e6,
             "kernel_ms_max_over_ranks": kern_ms_max,
             "rank_render_ms_after_rebalance": rank_ms_rebalanced if native else None,
+            "frame_check": frame_check,
             "host_path_ms_per_step": host_ms,
             "host_path": "rt_render into a host ARGB buffer (the JNI draw(), INTEGRATION.md): kernel + "
                          f"{W * H * 4} B read-back to pageable memory, blocking; 1-GPU runs only",
@@ -505,6 +536,8 @@ def main():
         print(json.dumps(out), flush=True)
     if native:
         grp.close()
+    if comm is not None:
+        comm.close()
     scene.close()
     if dist:
         dist.destroy_process_group()

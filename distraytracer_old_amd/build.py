@@ -8,6 +8,10 @@ public header, and the compiler flags (this file's settings). It is compiled in 
 and written next to the library (lib/libdistraytracer.buildinfo.json); a library whose id
 differs from the tree's is rebuilt, so a shipped .so is used only when it was built from these
 sources with these flags. build() reports whether it compiled or reused the library.
+
+Objects are cached by content (lib/obj/<source>.<hash>.o, the hash over the source, every header and
+the flags): a rebuild compiles only the translation units whose inputs changed. The build id itself is
+compiled into build_id.cpp alone.
 """
 from __future__ import annotations
 
@@ -24,12 +28,14 @@ LIB_PATH = LIB_DIR / "libdistraytracer.so"
 INFO_PATH = LIB_DIR / "libdistraytracer.buildinfo.json"
 PUBLIC_HEADER = PKG.parent / "include" / "distraytracer.h"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["trace.hip", "render_minreg.hip", "photon_build.hip", "group.hip", "cli_loader.cpp", "scene_build.cpp", "photon.cpp"]
+SOURCES = ["trace.hip", "render_minreg.hip", "photon_build.hip", "group.hip", "comm.hip", "cli_loader.cpp", "scene_build.cpp",
+           "photon.cpp", "build_id.cpp"]
+OBJ_DIR = LIB_DIR / "obj"
 # per-source compiler flags: render_minreg.hip holds C3's and C5's render variants, which run
 # faster with the register-minimising scheduler (C4's variant, in trace.hip, runs slower with it)
 SOURCE_FLAGS = {"render_minreg.hip": ["-Xarch_device", "-mllvm=--amdgpu-sched-strategy=iterative-minreg",
                                       "-Xarch_device", "-mllvm=--amdgpu-use-amdgpu-trackers=1"]}
-HEADERS = ["rt_types.h", "rt_internal.h", "host_math.h", "trace_device.h", "trace_kernels.h", "wavefront.h", "qdiv.h",
+HEADERS = ["rt_types.h", "rt_internal.h", "comm.h", "host_math.h", "trace_device.h", "trace_kernels.h", "wavefront.h", "qdiv.h",
            "jfdlibm.h"]
 # -ffp-contract=off: keep the reference's (Java) unfused double arithmetic so discrete
 # decisions (hits, shadows, TIR) match the oracle; no fast-math (IEEE Inf/NaN needed).
@@ -86,21 +92,31 @@ def build(force: bool = False, verbose: bool = False, defines: list[str] | None 
     bid = build_id(defines)
     target.parent.mkdir(parents=True, exist_ok=True)
     tmp = target.with_suffix(".so.tmp%d" % os.getpid())
-    tag = "" if out is None else target.stem + "."
     objs, procs = [], []
+    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    hdr = b"".join(p.name.encode() + b"\0" + p.read_bytes() for p in [CSRC / h for h in HEADERS] + [PUBLIC_HEADER])
     for src in SOURCES:  # .hip -> device+host; .cpp -> host-only C++ (no device pass); compiled in parallel
-        obj = target.parent / (tag + src + ".o")
         lang = [] if src.endswith(".hip") else ["-x", "c++"]
-        cmd = [HIPCC, *COMPILE_FLAGS, *SOURCE_FLAGS.get(src, []), *_extra_flags(src, defines), f'-DRT_BUILD_ID="{bid}"',
-               *lang, "-c", str(CSRC / src), "-o", str(obj)]
-        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)))
+        flags = [*COMPILE_FLAGS, *SOURCE_FLAGS.get(src, []), *_extra_flags(src, defines)]
+        if src == "build_id.cpp":
+            flags.append(f'-DRT_BUILD_ID="{bid}"')
+        key = hashlib.sha256((CSRC / src).read_bytes() + hdr + json.dumps([HIPCC, flags, lang]).encode()).hexdigest()[:16]
+        obj = OBJ_DIR / f"{src}.{key}.o"
         objs.append(str(obj))
+        if obj.exists() and not force:
+            continue
+        tmpo = obj.with_suffix(".o.tmp%d" % os.getpid())
+        cmd = [HIPCC, *flags, *lang, "-c", str(CSRC / src), "-o", str(tmpo)]
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True), tmpo, obj))
     logs, failed = [], None
-    for src, pr in procs:
+    for src, pr, tmpo, obj in procs:
         err = pr.communicate()[1]
         logs.append(err)
-        if pr.returncode != 0 and failed is None:
-            failed = f"hipcc failed on {src}:\n" + err[-4000:]
+        if pr.returncode != 0:
+            if failed is None:
+                failed = f"hipcc failed on {src}:\n" + err[-4000:]
+        else:
+            os.replace(tmpo, obj)
     if failed:
         raise RuntimeError(failed)
     r = subprocess.run([HIPCC, "-shared", "--offload-arch=gfx950", "-o", str(tmp), *objs, "-ldl"], capture_output=True, text=True)
@@ -109,6 +125,10 @@ def build(force: bool = False, verbose: bool = False, defines: list[str] | None 
     if verbose:
         print("\n".join(logs))
     os.replace(tmp, target)
+    for src in SOURCES:  # keep the newest few cached objects per source
+        old = sorted(OBJ_DIR.glob(f"{src}.*.o"), key=lambda q: q.stat().st_mtime, reverse=True)
+        for q in old[6:]:
+            q.unlink(missing_ok=True)
     if out is None:
         INFO_PATH.write_text(json.dumps({"build_id": bid, "defines": defines or []}) + "\n")
     last_action = "compiled"

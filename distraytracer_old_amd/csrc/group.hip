@@ -19,22 +19,23 @@
 // Pixels, their RNG keys and their per-pixel sample order do not depend on the plan, so the frame
 // equals the 1-GPU frame bit for bit for every N and transport.
 //
-// RCCL is loaded at run time (dlopen of librccl.so.1, which in a PyTorch process is the copy torch
-// already loaded), so the library and the COPY transport work without it.
+// Transports: RCCL (one device per rank; in one process ncclCommInitAll, one process per GPU an
+// rt_comm from rt_comm_create_rccl), the host transport of an rt_comm made by rt_comm_create_host
+// (caller callbacks on pinned host staging; ranks may share a device, so the rank-mode path runs as
+// N processes on one GPU), or device copies in one process (RT_GROUP_COPY, the one-GPU emulation).
+// In rank mode every collective carries the ranks' status so that all ranks fail together, and
+// every cut of the plan ends in a plan check: each sender's offset, pixel count and pixel-list hash
+// against the receive side rank 0 derives (plan_check).
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
-
-#include <dlfcn.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstring>
-#include <mutex>
 #include <string>
 #include <vector>
 
-#include "rt_internal.h"
+#include "comm.h"
 
 using namespace rt;
 
@@ -44,68 +45,6 @@ using namespace rt;
     if (e_ != hipSuccess)                                                                \
       return set_error(RT_E_HIP, std::string(#expr " failed: ") + hipGetErrorString(e_)); \
   } while (0)
-
-// ---------------------------------------------------------------------------------------------
-// RCCL, resolved at run time
-namespace {
-struct Rccl {
-  bool tried = false, ok = false;
-  std::string why;
-  decltype(&ncclGetUniqueId) getUniqueId = nullptr;
-  decltype(&ncclCommInitRank) commInitRank = nullptr;
-  decltype(&ncclCommInitAll) commInitAll = nullptr;
-  decltype(&ncclCommDestroy) commDestroy = nullptr;
-  decltype(&ncclGroupStart) groupStart = nullptr;
-  decltype(&ncclGroupEnd) groupEnd = nullptr;
-  decltype(&ncclSend) send = nullptr;
-  decltype(&ncclRecv) recv = nullptr;
-  decltype(&ncclBroadcast) bcast = nullptr;
-  decltype(&ncclAllGather) allGather = nullptr;
-  decltype(&ncclGetErrorString) errStr = nullptr;
-};
-Rccl g_rccl;
-std::mutex g_rccl_mu;
-
-int rccl_load() {
-  std::lock_guard<std::mutex> lk(g_rccl_mu);
-  Rccl& R = g_rccl;
-  if (!R.tried) {
-    R.tried = true;
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) {
-      R.why = std::string("cannot load librccl.so.1: ") + dlerror();
-    } else {
-      bool all = true;
-      auto sym = [&](auto& fn, const char* name) {
-        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
-        all = all && fn != nullptr;
-      };
-      sym(R.getUniqueId, "ncclGetUniqueId");
-      sym(R.commInitRank, "ncclCommInitRank");
-      sym(R.commInitAll, "ncclCommInitAll");
-      sym(R.commDestroy, "ncclCommDestroy");
-      sym(R.groupStart, "ncclGroupStart");
-      sym(R.groupEnd, "ncclGroupEnd");
-      sym(R.send, "ncclSend");
-      sym(R.recv, "ncclRecv");
-      sym(R.bcast, "ncclBroadcast");
-      sym(R.allGather, "ncclAllGather");
-      sym(R.errStr, "ncclGetErrorString");
-      R.ok = all;
-      if (!all) R.why = "librccl.so.1 lacks an entry point the group needs";
-    }
-  }
-  return R.ok ? RT_OK : set_error(RT_E_INVALID, "RCCL transport unavailable: " + R.why);
-}
-
-#define NCHK(expr)                                                                                   \
-  do {                                                                                               \
-    ncclResult_t r_ = (expr);                                                                        \
-    if (r_ != ncclSuccess)                                                                           \
-      return set_error(RT_E_HIP, std::string(#expr " failed: ") + g_rccl.errStr(r_));               \
-  } while (0)
-}  // namespace
 
 // ---------------------------------------------------------------------------------------------
 // plan (host only; multigpu.py rank_plans is the independent Python restatement the tests compare)
@@ -214,7 +153,7 @@ struct GRank {
   hipEvent_t evStart = nullptr, evSide = nullptr, evPacked = nullptr, evSent[2] = {}, evRendered = nullptr;
   hipEvent_t tA[KRING] = {}, tB[KRING] = {};
   int64_t timed = 0;  // frames with kernel events since the last rt_group_kernel_ms
-  ncclComm_t comm = nullptr;
+  ncclComm_t nccl = nullptr;  // RCCL transport: this rank's communicator (rank mode: the rt_comm's, borrowed)
   int64_t off = 0;  // offset of this rank's pixels in rank 0's receive slab
 };
 }  // namespace
@@ -222,6 +161,13 @@ struct GRank {
 struct rt_group {
   int world = 1;
   bool rankMode = false, useRccl = false, rgb = false, root = false;
+  bool hostX = false;        // rank mode over a host-transport rt_comm: the exchange staged through pinned memory
+  rt_comm* comm = nullptr;   // rank mode at world > 1 (owned when ownComm: rt_group_create_rank)
+  bool ownComm = false;
+  int64_t planChecks = 0;    // collective plan checks passed (plan_check)
+  std::vector<uint64_t> pixHash;  // per rank: hash of the pixel list it sends (rank_lists `all`)
+  char* hSend = nullptr;     // host transport: pinned staging of this rank's packed pixels / rank 0's slab
+  char* hRecv = nullptr;
   uint32_t renderFlags = 0;
   rt_render_params p{};
   int W = 0, H = 0, ntiles = 0, tilesX = 0, tw = 0, th = 0;
@@ -246,6 +192,7 @@ struct rt_group {
   int64_t frame = 0;
   std::vector<void*> allocs;      // for the group's life (streams' frames, rank 0's output)
   std::vector<void*> planAllocs;  // per plan (setup_lists; freed when rt_group_rebalance re-cuts)
+  std::vector<void*> planHost;    // per plan, pinned host (hSend / hRecv)
 };
 
 namespace {
@@ -328,21 +275,45 @@ int setup_streams(rt_group* g) {
   return RT_OK;
 }
 
+// FNV-1a of a pixel list (plan_check compares the lists the ranks derive without sending them)
+uint64_t hash_list(const std::vector<int32_t>& v) {
+  uint64_t h = 1469598103934665603ull ^ (uint64_t)v.size();
+  for (int32_t x : v) {
+    h ^= (uint32_t)x;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+// rank 0's receive offset of rank q's pixels: the slab holds ranks 1, 2, ... in rank order (the RCCL
+// and host receive loops); a sender's own R.off comes from setup_lists, and plan_check compares them
+int64_t recv_offset(const rt_group* g, int q) {
+  int64_t o = 0;
+  for (int k = 1; k < q; ++k) o += g->npix[k];
+  return o;
+}
+
 // per plan (again after rt_group_rebalance): the ranks' tile / pixel lists on the device, their
-// sample buffers and send slabs, rank 0's scatter list and receive slabs
-int setup_lists(rt_group* g) {
-  if (!g->planAllocs.empty()) {  // a re-cut: the previous plan's buffers, once no stream uses them
+// sample buffers and send slabs, rank 0's scatter list and receive slabs (this process's ranks only;
+// plan_check makes it collective in rank mode)
+int setup_lists_local(rt_group* g) {
+  if (!g->planAllocs.empty() || !g->planHost.empty()) {  // a re-cut: the previous plan's buffers, once no stream uses them
     int rc0 = sync_group(g);
     if (rc0) return rc0;
     for (void* p : g->planAllocs) GCHK(hipFree(p));
+    for (void* p : g->planHost) GCHK(hipHostFree(p));
     g->planAllocs.clear();
+    g->planHost.clear();
+    g->hSend = g->hRecv = nullptr;
   }
   g->npix.assign(g->world, 0);
+  g->pixHash.assign(g->world, 0);
   {
     std::vector<int32_t> a, b, c, d;
     for (int q = 0; q < g->world; ++q) {
       rank_lists(g, q, a, b, c, d);
       g->npix[q] = (int64_t)d.size();
+      g->pixHash[q] = hash_list(d);
     }
   }
   int64_t off = 0;
@@ -380,12 +351,58 @@ int setup_lists(rt_group* g) {
       if (g->rgb && (rc = gmalloc(g, (void**)&g->rRgb[b2], g->nRecv * 3 * sizeof(float), true))) return rc;
     }
   }
+  if (g->hostX) {  // pinned staging of the host transport: a sender's packed pixels, rank 0's whole slab
+    const size_t px = sizeof(int32_t) + (g->rgb ? 3 * sizeof(float) : 0);
+    const GRank& R = g->r[0];
+    const size_t bytes = R.rank == 0 ? (size_t)g->nRecv * px : R.hAll.size() * px;
+    if (bytes) {
+      void* h = nullptr;
+      GCHK(hipHostMalloc(&h, bytes));
+      g->planHost.push_back(h);
+      (R.rank == 0 ? g->hRecv : g->hSend) = (char*)h;
+    }
+  }
   return RT_OK;
 }
 
+// Rank mode, world > 1: every rank's {status, rank, offset in rank 0's slab, pixel count, pixel-list
+// hash, plan hash} all-gathered and checked by every rank against its own derivation of the plan --
+// the receive offsets and counts rank 0's receive loop uses (recv_offset, npix) and the pixel lists
+// (pixHash). A rank's local failure or any disagreement fails every rank here, before a frame
+// exchange could block on a mismatched send / receive.
+int plan_check(rt_group* g, int local_rc) {
+  if (!g->rankMode || g->world == 1 || !g->comm) return local_rc;
+  const std::string mine = local_rc ? std::string(rt_last_error()) : std::string();
+  uint64_t plan = hash_list(g->owner) ^ (hash_list(g->order) * 31);
+  const GRank* R = g->r.empty() ? nullptr : &g->r[0];
+  const int64_t rec[6] = {local_rc, R ? R->rank : -1, R ? R->off : -1, R ? (int64_t)R->hAll.size() : -1,
+                          (int64_t)(local_rc || !R ? 0 : g->pixHash[R->rank]), (int64_t)plan};
+  std::vector<int64_t> all(6 * (size_t)g->world);
+  int rc = comm_allgather(g->comm, rec, all.data(), sizeof(rec));
+  if (rc) return rc;
+  if (local_rc) return set_error(local_rc, mine);
+  for (int q = 0; q < g->world; ++q) {
+    const int64_t* x = &all[6 * (size_t)q];
+    if (x[0]) return set_error((int)x[0], "rt_group: rank " + std::to_string(q) + " failed its setup; every rank stops");
+    std::string why;
+    if (x[1] != q) why = "reports rank " + std::to_string(x[1]);
+    else if (x[5] != (int64_t)plan) why = "derived a different plan (owner / order)";
+    else if (q > 0 && x[2] != recv_offset(g, q))
+      why = "sends at offset " + std::to_string(x[2]) + " of rank 0's slab, rank 0 receives it at " + std::to_string(recv_offset(g, q));
+    else if (x[3] != g->npix[q]) why = "sends " + std::to_string(x[3]) + " pixels, rank 0 receives " + std::to_string(g->npix[q]);
+    else if (x[4] != (int64_t)g->pixHash[q]) why = "sends a different pixel list";
+    if (!why.empty()) return set_error(RT_E_INVALID, "rt_group plan check: rank " + std::to_string(q) + " " + why);
+  }
+  g->planChecks++;
+  return RT_OK;
+}
+
+int setup_lists(rt_group* g) { return plan_check(g, setup_lists_local(g)); }
+
 int setup_ranks(rt_group* g) {
   int rc = setup_streams(g);
-  return rc ? rc : setup_lists(g);
+  if (rc == RT_OK) rc = setup_lists_local(g);
+  return plan_check(g, rc);
 }
 
 int make_layout(rt_group* g, rt_scene* s, const rt_render_params* p, uint32_t flags) {
@@ -495,29 +512,68 @@ int group_frame(rt_group* g, float* rgb, int32_t* argb) {
         GCHK(hipSetDevice(R0->dev));
         GCHK(hipStreamWaitEvent(R0->cs, g->evRecv[b], 0));
       }
-      NCHK(g_rccl.groupStart());
+      // a failed call inside the group is recorded and the group still closed (an open group
+      // would leave every later RCCL call of this thread queued)
+      ncclResult_t first = g_rccl.groupStart();
+      if (first != ncclSuccess) return set_error(RT_E_HIP, std::string("ncclGroupStart failed: ") + g_rccl.errStr(first));
+      auto keep = [&](ncclResult_t r) {
+        if (first == ncclSuccess) first = r;
+      };
       for (GRank& R : g->r) {
         const size_t n = R.hAll.size();
         if (R.rank != 0 && n) {
-          NCHK(g_rccl.send(R.sArgb[b], n, ncclInt32, 0, R.comm, R.cs));
-          if (g->rgb) NCHK(g_rccl.send(R.sRgb[b], 3 * n, ncclFloat32, 0, R.comm, R.cs));
+          keep(g_rccl.send(R.sArgb[b], n, ncclInt32, 0, R.nccl, R.cs));
+          if (g->rgb) keep(g_rccl.send(R.sRgb[b], 3 * n, ncclFloat32, 0, R.nccl, R.cs));
         }
       }
       if (R0)
         for (int q = 1; q < g->world; ++q) {
-          int64_t o = 0;
-          for (int k = 1; k < q; ++k) o += g->npix[k];
+          const int64_t o = recv_offset(g, q);
           const size_t n = (size_t)g->npix[q];
           if (!n) continue;
-          NCHK(g_rccl.recv(g->rArgb[b] + o, n, ncclInt32, q, R0->comm, R0->cs));
-          if (g->rgb) NCHK(g_rccl.recv(g->rRgb[b] + 3 * o, 3 * n, ncclFloat32, q, R0->comm, R0->cs));
+          keep(g_rccl.recv(g->rArgb[b] + o, n, ncclInt32, q, R0->nccl, R0->cs));
+          if (g->rgb) keep(g_rccl.recv(g->rRgb[b] + 3 * o, 3 * n, ncclFloat32, q, R0->nccl, R0->cs));
         }
-      NCHK(g_rccl.groupEnd());
+      keep(g_rccl.groupEnd());
+      if (first != ncclSuccess) return set_error(RT_E_HIP, std::string("RCCL frame exchange failed: ") + g_rccl.errStr(first));
       for (GRank& R : g->r)
         if (R.rank != 0) {
           GCHK(hipSetDevice(R.dev));
           GCHK(hipEventRecord(R.evSent[b], R.cs));
         }
+    } else if (g->hostX) {
+      // host transport (rank mode, one rank in this process): blocking, staged through pinned memory
+      GRank& R = g->r[0];
+      GCHK(hipSetDevice(R.dev));
+      const size_t ab = sizeof(int32_t), cb = 3 * sizeof(float);
+      if (R.rank != 0) {
+        const size_t n = R.hAll.size();
+        if (n) {
+          GCHK(hipMemcpyAsync(g->hSend, R.sArgb[b], n * ab, hipMemcpyDeviceToHost, R.cs));
+          if (g->rgb) GCHK(hipMemcpyAsync(g->hSend + n * ab, R.sRgb[b], n * cb, hipMemcpyDeviceToHost, R.cs));
+        }
+        GCHK(hipEventRecord(R.evSent[b], R.cs));
+        GCHK(hipStreamSynchronize(R.cs));
+        if (n && ((rc = comm_send(g->comm, g->hSend, n * ab, 0)) ||
+                  (g->rgb && (rc = comm_send(g->comm, g->hSend + n * ab, n * cb, 0)))))
+          return rc;
+      } else {
+        // the previous frame's upload from hRecv has finished once cs is idle; slab b's last scatter
+        // is ordered before this frame's upload by evRecv[b]
+        GCHK(hipStreamSynchronize(R.cs));
+        for (int q = 1; q < g->world; ++q) {
+          const int64_t o = recv_offset(g, q);
+          const size_t n = (size_t)g->npix[q];
+          if (!n) continue;
+          if ((rc = comm_recv(g->comm, g->hRecv + o * ab, n * ab, q))) return rc;
+          if (g->rgb && (rc = comm_recv(g->comm, g->hRecv + g->nRecv * ab + o * cb, n * cb, q))) return rc;
+        }
+        GCHK(hipStreamWaitEvent(R.cs, g->evRecv[b], 0));
+        if (g->nRecv) {
+          GCHK(hipMemcpyAsync(g->rArgb[b], g->hRecv, g->nRecv * ab, hipMemcpyHostToDevice, R.cs));
+          if (g->rgb) GCHK(hipMemcpyAsync(g->rRgb[b], g->hRecv + g->nRecv * ab, g->nRecv * cb, hipMemcpyHostToDevice, R.cs));
+        }
+      }
     } else {
       // one process: device copies of every rank's packed pixels into rank 0's receive slab
       GCHK(hipSetDevice(R0->dev));
@@ -573,7 +629,7 @@ int destroy_group(rt_group* g) {
   }
   for (GRank& R : g->r) {
     (void)hipSetDevice(R.dev);
-    if (R.comm && g_rccl.ok) (void)g_rccl.commDestroy(R.comm);
+    if (R.nccl && !g->rankMode && g_rccl.ok) (void)g_rccl.commDestroy(R.nccl);  // rank mode: the rt_comm's
     for (hipEvent_t e : {R.evStart, R.evSide, R.evPacked, R.evRendered, R.evSent[0], R.evSent[1]})
       if (e) (void)hipEventDestroy(e);
     for (int k = 0; k < KRING; ++k) {
@@ -590,7 +646,9 @@ int destroy_group(rt_group* g) {
     if (e) (void)hipEventDestroy(e);
   for (void* p : g->allocs) (void)hipFree(p);
   for (void* p : g->planAllocs) (void)hipFree(p);
+  for (void* p : g->planHost) (void)hipHostFree(p);
   if (g->stage) (void)hipHostFree(g->stage);
+  if (g->ownComm) rt_comm_destroy(g->comm);
   delete g;
   return RT_OK;
 }
@@ -613,7 +671,8 @@ int rt_group_unique_id(void* id, int cap) {
   int rc = rccl_load();
   if (rc) return rc;
   ncclUniqueId u;
-  NCHK(g_rccl.getUniqueId(&u));
+  const ncclResult_t nr = g_rccl.getUniqueId(&u);
+  if (nr != ncclSuccess) return set_error(RT_E_HIP, std::string("ncclGetUniqueId failed: ") + g_rccl.errStr(nr));
   std::memcpy(id, &u, sizeof(u));
   return (int)sizeof(u);
 }
@@ -622,6 +681,7 @@ int rt_group_create(rt_scene* const* scenes, int n, const rt_render_params* p, u
                     rt_group** out) {
   if (!scenes || n < 1 || !out) return set_error(RT_E_INVALID, "rt_group_create: bad arguments");
   *out = nullptr;
+  DeviceGuard dg;
   for (int i = 0; i < n; ++i)
     if (!scenes[i]) return set_error(RT_E_INVALID, "rt_group_create: null scene");
   const bool rccl = n > 1 && !(flags & RT_GROUP_COPY);
@@ -662,7 +722,85 @@ int rt_group_create(rt_scene* const* scenes, int n, const rt_render_params* p, u
     ncclResult_t nr = g_rccl.commInitAll(comms.data(), n, devs.data());
     if (nr != ncclSuccess) rc = set_error(RT_E_HIP, std::string("ncclCommInitAll failed: ") + g_rccl.errStr(nr));
     else
-      for (int i = 0; i < n; ++i) g->r[i].comm = comms[i];
+      for (int i = 0; i < n; ++i) g->r[i].nccl = comms[i];
+  }
+  if (rc != RT_OK) {
+    const std::string msg = rt_last_error();
+    destroy_group(g);
+    return set_error(rc, msg);
+  }
+  *out = g;
+  return RT_OK;
+}
+
+int rt_group_create_comm(rt_scene* scene, rt_comm* comm, const rt_render_params* p, uint32_t flags, double heavy,
+                         int slots, rt_group** out) {
+  if (!scene || !out) return set_error(RT_E_INVALID, "rt_group_create_comm: bad arguments");
+  *out = nullptr;
+  DeviceGuard dg;
+  const int world = comm ? comm->world : 1, rank = comm ? comm->rank : 0;
+  if (flags & RT_GROUP_COPY) return set_error(RT_E_INVALID, "rt_group_create_comm: RT_GROUP_COPY is a one-process transport");
+  rt_group* g = new rt_group();
+  g->world = world;
+  g->rankMode = true;
+  g->comm = world > 1 ? comm : nullptr;
+  g->useRccl = world > 1 && comm->rccl;
+  g->hostX = world > 1 && !comm->rccl;
+  g->root = rank == 0;
+  g->rootDev = scene->device;
+  int rc = (g->useRccl && comm->device != scene->device)
+               ? set_error(RT_E_INVALID, "rt_group_create_comm: the RCCL communicator is on device " +
+                                             std::to_string(comm->device) + ", the scene on " + std::to_string(scene->device))
+               : RT_OK;
+  if (rc == RT_OK) rc = make_layout(g, scene, p, flags);
+  if (rc == RT_OK && !(heavy > 0)) heavy = 1.25;
+  if (rc == RT_OK && slots <= 0) slots = 4096;
+  // 1. the ranks were given the same frame (a mismatch would size the collectives differently)
+  if (g->comm) {
+    int64_t hb;
+    std::memcpy(&hb, &heavy, sizeof(hb));
+    const int64_t mine[10] = {rc, g->W, g->H, g->p.spp, (int64_t)g->p.seed, g->p.flags, hb, slots, g->ntiles, g->rgb};
+    const std::string myMsg = rc ? std::string(rt_last_error()) : std::string();
+    std::vector<int64_t> all(10 * (size_t)world);
+    int rc2 = comm_allgather(g->comm, mine, all.data(), sizeof(mine));
+    if (rc2 == RT_OK && rc) rc2 = set_error(rc, myMsg);
+    for (int q = 0; q < world && rc2 == RT_OK; ++q) {
+      const int64_t* x = &all[10 * (size_t)q];
+      if (x[0]) rc2 = set_error((int)x[0], "rt_group_create_comm: rank " + std::to_string(q) + " failed its setup");
+      else if (std::memcmp(x + 1, mine + 1, 9 * sizeof(int64_t)))
+        rc2 = set_error(RT_E_INVALID, "rt_group_create_comm: rank " + std::to_string(q) +
+                                          " was given a different frame (size / spp / seed / flags / heavy / slots)");
+    }
+    rc = rc2;
+  }
+  // 2. rank 0 measures the layout's wave times; every rank receives them behind rank 0's status
+  std::vector<uint32_t> cost;
+  if (rc == RT_OK) {
+    cost.assign(g->ntiles + 1, 1);
+    cost[0] = 0;
+    if (rank == 0) {
+      const int m = rt_tile_costs(scene, &g->p, cost.data() + 1, g->ntiles);
+      const int crc = m < 0 ? m : (m != g->ntiles ? set_error(RT_E_INVALID, "rt_group_create_comm: tile count mismatch") : RT_OK);
+      cost[0] = (uint32_t)crc;
+      if (crc) std::fill(cost.begin() + 1, cost.end(), 1u);
+    }
+    const std::string msg0 = cost[0] ? std::string(rt_last_error()) : std::string();
+    if (g->comm) rc = comm_bcast(g->comm, cost.data(), cost.size() * sizeof(uint32_t), 0);
+    if (rc == RT_OK && cost[0])
+      rc = rank == 0 ? set_error((int)(int32_t)cost[0], msg0)
+                     : set_error((int)(int32_t)cost[0], "rt_group_create_comm: rank 0 failed to calibrate the layout");
+    cost.erase(cost.begin());
+  }
+  // 3. the plan (deterministic: every rank derives the same one) and this rank's lists, checked
+  if (rc == RT_OK) rc = make_plan(g, cost, heavy, slots);
+  if (rc == RT_OK) {
+    GRank R;
+    R.s = scene;
+    R.dev = scene->device;
+    R.rank = rank;
+    R.nccl = g->useRccl ? comm->nccl : nullptr;
+    g->r.push_back(R);
+    rc = setup_ranks(g);  // collective (plan_check)
   }
   if (rc != RT_OK) {
     const std::string msg = rt_last_error();
@@ -678,82 +816,36 @@ int rt_group_create_rank(rt_scene* scene, int rank, int world, const void* uniqu
   if (!scene || !out || world < 1 || rank < 0 || rank >= world || (world > 1 && !unique_id))
     return set_error(RT_E_INVALID, "rt_group_create_rank: bad arguments");
   *out = nullptr;
+  rt_comm* c = nullptr;
   if (world > 1) {
-    int rc = rccl_load();
+    int rc = rt_comm_create_rccl(rank, world, unique_id, scene->device, &c);
     if (rc) return rc;
   }
-  rt_group* g = new rt_group();
-  g->world = world;
-  g->rankMode = true;
-  g->useRccl = world > 1;
-  g->root = rank == 0;
-  g->rootDev = scene->device;
-  int rc = make_layout(g, scene, p, flags);
-  GRank R;
-  R.s = scene;
-  R.dev = scene->device;
-  R.rank = rank;
-  if (rc == RT_OK && world > 1) {
-    ncclUniqueId u;
-    std::memcpy(&u, unique_id, sizeof(u));
-    hipError_t he = hipSetDevice(R.dev);
-    if (he != hipSuccess) rc = set_error(RT_E_HIP, hipGetErrorString(he));
-    ncclResult_t nr = rc ? ncclSuccess : g_rccl.commInitRank(&R.comm, world, u, rank);
-    if (nr != ncclSuccess) rc = set_error(RT_E_HIP, std::string("ncclCommInitRank failed: ") + g_rccl.errStr(nr));
-  }
-  std::vector<uint32_t> cost;
-  if (rc == RT_OK) {  // rank 0 measures the layout's wave times; every rank receives them
-    cost.assign(g->ntiles, 1);
-    if (rank == 0) {
-      const int m = rt_tile_costs(scene, &g->p, cost.data(), g->ntiles);
-      rc = m < 0 ? m : (m != g->ntiles ? set_error(RT_E_INVALID, "rt_group_create_rank: tile count mismatch") : RT_OK);
-    }
-    if (world > 1) {  // (every rank reaches the broadcast: a failed calibration sends unit costs, then reports)
-      uint32_t* d = nullptr;
-      hipStream_t st = nullptr;
-      hipError_t he = hipSetDevice(R.dev);
-      if (he == hipSuccess) he = hipMalloc(&d, sizeof(uint32_t) * g->ntiles);
-      if (he == hipSuccess) he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-      if (he == hipSuccess) he = hipMemcpy(d, cost.data(), sizeof(uint32_t) * g->ntiles, hipMemcpyHostToDevice);
-      ncclResult_t nr = ncclSuccess;
-      if (he == hipSuccess) nr = g_rccl.bcast(d, d, (size_t)g->ntiles, ncclUint32, 0, R.comm, st);
-      if (he == hipSuccess && nr == ncclSuccess) he = hipStreamSynchronize(st);
-      if (he == hipSuccess && nr == ncclSuccess) he = hipMemcpy(cost.data(), d, sizeof(uint32_t) * g->ntiles, hipMemcpyDeviceToHost);
-      if (st) (void)hipStreamDestroy(st);
-      if (d) (void)hipFree(d);
-      if (rc == RT_OK && he != hipSuccess) rc = set_error(RT_E_HIP, std::string("cost broadcast: ") + hipGetErrorString(he));
-      if (rc == RT_OK && nr != ncclSuccess) rc = set_error(RT_E_HIP, std::string("cost broadcast: ") + g_rccl.errStr(nr));
-    }
-  }
-  if (rc == RT_OK) rc = make_plan(g, cost, heavy, slots);
-  if (rc == RT_OK) {
-    g->r.push_back(R);
-    R.comm = nullptr;  // owned by g->r[0] now
-    rc = setup_ranks(g);
-  } else if (R.comm) {
-    (void)g_rccl.commDestroy(R.comm);
-  }
-  if (rc != RT_OK) {
+  int rc = rt_group_create_comm(scene, c, p, flags, heavy, slots, out);
+  if (rc) {
     const std::string msg = rt_last_error();
-    destroy_group(g);
+    rt_comm_destroy(c);
     return set_error(rc, msg);
   }
-  *out = g;
+  (*out)->ownComm = c != nullptr;
   return RT_OK;
 }
 
 int rt_group_render(rt_group* g, float* d_rgb, int32_t* d_argb) {
   if (!g) return set_error(RT_E_INVALID, "rt_group_render: null group");
+  DeviceGuard dg;
   return group_frame(g, d_rgb, d_argb);
 }
 
 int rt_group_sync(rt_group* g) {
   if (!g) return set_error(RT_E_INVALID, "rt_group_sync: null group");
+  DeviceGuard dg;
   return sync_group(g);
 }
 
 int rt_group_render_host(rt_group* g, float* rgb, int32_t* argb) {
   if (!g) return set_error(RT_E_INVALID, "rt_group_render_host: null group");
+  DeviceGuard dg;
   if (rgb && !g->rgb) return set_error(RT_E_INVALID, "rt_group_render_host: float-RGB output needs RT_GROUP_RGB");
   int rc = group_frame(g, g->root ? g->outRgb : nullptr, g->root ? g->outArgb : nullptr);
   if (rc) return rc;
@@ -781,9 +873,9 @@ int rt_group_frame(rt_group* g, float** d_rgb, int32_t** d_argb) {
 
 int rt_group_info(const rt_group* g, int64_t* info, int n) {
   if (!g || !info) return set_error(RT_E_INVALID, "rt_group_info: null argument");
-  const int64_t v[9] = {g->world, (int64_t)g->r.size(), g->r.empty() ? -1 : g->r[0].rank, g->ntiles, g->tilesX, g->tw,
-                        g->th, g->useRccl ? 1 : 0, g->frame};
-  for (int i = 0; i < n && i < 9; ++i) info[i] = v[i];
+  const int64_t v[10] = {g->world, (int64_t)g->r.size(), g->r.empty() ? -1 : g->r[0].rank, g->ntiles, g->tilesX, g->tw,
+                         g->th, g->useRccl ? 1 : (g->hostX ? 2 : 0), g->frame, g->planChecks};
+  for (int i = 0; i < n && i < 10; ++i) info[i] = v[i];
   return RT_OK;
 }
 
@@ -806,6 +898,7 @@ int rt_group_rank_pixels(const rt_group* g, int rank, int32_t* pixels, int64_t c
 
 int rt_group_kernel_ms(rt_group* g, int rank, double* avg_ms, int* frames) {
   if (!g || !avg_ms) return set_error(RT_E_INVALID, "rt_group_kernel_ms: null argument");
+  DeviceGuard dg;
   GRank* R = local_rank(g, rank);
   if (!R) return set_error(RT_E_INVALID, "rt_group_kernel_ms: rank not driven by this process");
   GCHK(hipSetDevice(R->dev));
@@ -830,6 +923,7 @@ int rt_group_kernel_ms(rt_group* g, int rank, double* avg_ms, int* frames) {
 // mean HIP-event time of its render.
 int rt_group_time_rank(rt_group* g, int rank, int warmup, int iters, double* step_ms, double* kernel_ms) {
   if (!g || iters <= 0 || !step_ms || !kernel_ms) return set_error(RT_E_INVALID, "rt_group_time_rank: bad arguments");
+  DeviceGuard dg;
   if (g->rankMode || g->useRccl) return set_error(RT_E_INVALID, "rt_group_time_rank: one-process RT_GROUP_COPY groups only");
   GRank* R = local_rank(g, rank);
   GRank* R0 = local_rank(g, 0);
@@ -894,36 +988,46 @@ int rt_group_count(rt_group* g, int rank, uint64_t* stats) {
 // render times of the last measurement, taken after the last cut.
 int rt_group_rebalance(rt_group* g, int rounds, int iters, double* rank_ms) {
   if (!g || rounds < 0 || iters <= 0) return set_error(RT_E_INVALID, "rt_group_rebalance: bad arguments");
+  DeviceGuard dg;
   if (g->weight.empty()) g->weight.assign(g->ntiles, 1.0);
   std::vector<double> T(g->world, 0.0);
-  int rc;
+  const bool coll = g->rankMode && g->world > 1 && g->comm;
   for (int round = 0; round <= rounds; ++round) {
-    if ((rc = sync_group(g))) return rc;
-    for (GRank& R : g->r) {  // each rank alone (one-process groups share devices), after 3 untimed frames
-      const bool r0 = R.rank == 0;
-      for (int i = 0; i < 3; ++i)
-        if ((rc = enqueue_render(g, R, r0 ? g->outRgb : R.fRgb, r0 ? g->outArgb : R.fArgb, false))) return rc;
-      GCHK(hipSetDevice(R.dev));
-      GCHK(hipStreamSynchronize(R.st));
-      R.timed = 0;
-      for (int i = 0; i < iters; ++i)
-        if ((rc = enqueue_render(g, R, r0 ? g->outRgb : R.fRgb, r0 ? g->outArgb : R.fArgb, true))) return rc;
-      int fr = 0;
-      if ((rc = rt_group_kernel_ms(g, R.rank, &T[R.rank], &fr))) return rc;
-    }
-    if (g->rankMode && g->world > 1) {  // every rank's time to every rank
-      GRank& R = g->r[0];
-      double* d = nullptr;
-      GCHK(hipSetDevice(R.dev));
-      GCHK(hipMalloc(&d, sizeof(double) * (g->world + 1)));
-      hipError_t he = hipMemcpy(d + g->world, &T[R.rank], sizeof(double), hipMemcpyHostToDevice);
-      ncclResult_t nr = ncclSuccess;
-      if (he == hipSuccess) nr = g_rccl.allGather(d + g->world, d, 1, ncclFloat64, R.comm, R.cs);
-      if (he == hipSuccess && nr == ncclSuccess) he = hipStreamSynchronize(R.cs);
-      if (he == hipSuccess && nr == ncclSuccess) he = hipMemcpy(T.data(), d, sizeof(double) * g->world, hipMemcpyDeviceToHost);
-      (void)hipFree(d);
-      if (he != hipSuccess) return set_error(RT_E_HIP, std::string("rebalance all-gather: ") + hipGetErrorString(he));
-      if (nr != ncclSuccess) return set_error(RT_E_HIP, std::string("rebalance all-gather: ") + g_rccl.errStr(nr));
+    // this process's ranks, each alone (one-process groups share devices), after 3 untimed frames;
+    // in rank mode a local failure is carried into the all-gather below instead of returning early
+    auto time_ranks = [&]() -> int {
+      int rc = sync_group(g);
+      if (rc) return rc;
+      for (GRank& R : g->r) {
+        const bool r0 = R.rank == 0;
+        for (int i = 0; i < 3; ++i)
+          if ((rc = enqueue_render(g, R, r0 ? g->outRgb : R.fRgb, r0 ? g->outArgb : R.fArgb, false))) return rc;
+        GCHK(hipSetDevice(R.dev));
+        GCHK(hipStreamSynchronize(R.st));
+        R.timed = 0;
+        for (int i = 0; i < iters; ++i)
+          if ((rc = enqueue_render(g, R, r0 ? g->outRgb : R.fRgb, r0 ? g->outArgb : R.fArgb, true))) return rc;
+        int fr = 0;
+        if ((rc = rt_group_kernel_ms(g, R.rank, &T[R.rank], &fr))) return rc;
+      }
+      return RT_OK;
+    };
+    int rc = time_ranks();
+    if (coll) {  // every rank's {status, time} to every rank
+      const std::string mine = rc ? std::string(rt_last_error()) : std::string();
+      const GRank& R = g->r[0];
+      double rec[2] = {(double)rc, T[R.rank]};
+      std::vector<double> all(2 * (size_t)g->world);
+      int rc2 = comm_allgather(g->comm, rec, all.data(), sizeof(rec));
+      if (rc2) return rc2;
+      if (rc) return set_error(rc, mine);
+      for (int q = 0; q < g->world; ++q) {
+        if (all[2 * q] != 0)
+          return set_error((int)all[2 * q], "rt_group_rebalance: rank " + std::to_string(q) + " failed to time its render");
+        T[q] = all[2 * q + 1];
+      }
+    } else if (rc) {
+      return rc;
     }
     if (round == rounds) break;
     // a rank's time per unit of weighted cost, relative to the frame's
@@ -936,17 +1040,21 @@ int rt_group_rebalance(rt_group* g, int rounds, int iters, double* rank_ms) {
     for (int q = 0; q < g->world; ++q)
       if (C[q] > 0 && T[q] > 0) f[q] = std::pow((T[q] / Tsum) / (C[q] / Csum), 0.75);
     for (int t = 0; t < g->ntiles; ++t) g->weight[t] *= f[g->owner[t] % g->world];
-    if ((rc = make_plan(g, g->cost, g->heavy, g->slots)) || (rc = setup_lists(g))) return rc;
+    if ((rc = make_plan(g, g->cost, g->heavy, g->slots)) || (rc = setup_lists(g))) return rc;  // setup_lists: collective check
   }
   if (rank_ms)
     for (int q = 0; q < g->world; ++q) rank_ms[q] = T[q];
   return RT_OK;
 }
 
-void rt_group_destroy(rt_group* g) { (void)destroy_group(g); }
+void rt_group_destroy(rt_group* g) {
+  DeviceGuard dg;
+  (void)destroy_group(g);
+}
 
 int rt_group_rccl_selftest(int device, int n) {
   if (n < 1) return set_error(RT_E_INVALID, "rt_group_rccl_selftest: n < 1");
+  DeviceGuard dg;
   int rc = rccl_load();
   if (rc) return rc;
   GCHK(hipSetDevice(device));

@@ -83,6 +83,14 @@ int launch_tile_list(rt_scene* s, const ParamsD& P, uint32_t flags, const int32_
                      int32_t* argb, void* stream);
 int launch_pixel_list(rt_scene* s, const ParamsD& P, uint32_t flags, const int32_t* dpix, int npix, double* smpCol,
                       uint8_t* smpTr, float* rgb, int32_t* argb, void* stream);
+// trace.hip: the photon pre-pass pieces comm.hip's sharded builds (rt_photons_build_comm / _local)
+// share with rt_photons_build: the scene's photon parameters checked; emitted photons [first,
+// first+count) of every light shot into pos / pwr (photon_list order, perLight[L] their counts per
+// light); the photon map built from a whole photon_list (pos / pwr are consumed)
+int check_photon_params(const HostScene& h);
+int shoot_photons(rt_scene* s, uint64_t seed, int64_t first, int64_t count, std::vector<double>& pos,
+                  std::vector<double>& pwr, std::vector<int64_t>& perLight);
+int set_photon_map(rt_scene* s, std::vector<double>& pos, std::vector<double>& pwr);
 // group.hip: the deterministic rank plan (rt_rank_plan)
 void plan_ranks(const uint32_t* cost, int n, int world, double heavy, int slots, int32_t* owner, int32_t* order,
                 const double* weight = nullptr);

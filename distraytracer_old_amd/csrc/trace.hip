@@ -317,10 +317,6 @@ int rt_upload_photons(rt_scene* s) {  // after the host photon-map build (csrc/p
 extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
-#ifndef RT_BUILD_ID
-#define RT_BUILD_ID "unknown"  // set by distraytracer_old_amd/build.py
-#endif
-const char* rt_build_id(void) { return RT_BUILD_ID; }
 const char* rt_last_error(void) { return g_last_error.c_str(); }
 
 int rt_device_count(int* count) {
@@ -1288,8 +1284,8 @@ int rt_upload_photons(rt_scene* s);
 // sendDiffusePhotons :1000-1091 with the emitted-photon index range restricted) into
 // pos/pwr in photon_list order: light, photon index, path slot. Chunked so the
 // per-lane slot buffers stay bounded for any photon count.
-static int shoot_photons(rt_scene* s, uint64_t seed, int64_t first, int64_t count, std::vector<double>& pos,
-                         std::vector<double>& pwr, std::vector<int64_t>& perLight) {
+int rt::shoot_photons(rt_scene* s, uint64_t seed, int64_t first, int64_t count, std::vector<double>& pos,
+                      std::vector<double>& pwr, std::vector<int64_t>& perLight) {
   HostScene& h = s->hs;
   pos.clear();
   pwr.clear();
@@ -1334,7 +1330,7 @@ static int shoot_photons(rt_scene* s, uint64_t seed, int64_t first, int64_t coun
   return RT_OK;
 }
 
-static int check_photon_params(const HostScene& h) {
+int rt::check_photon_params(const HostScene& h) {
   if (h.photonMode == 0) return set_error(RT_E_INVALID, "scene has no photon map");
   if (h.photonCount <= 0 || h.photonK <= 0) return set_error(RT_E_INVALID, "bad photon parameters");
   if (h.photonK > dv::KNN_MAX) return set_error(RT_E_INVALID, "photon neighbourhood k > 256 unsupported");
@@ -1344,7 +1340,7 @@ static int check_photon_params(const HostScene& h) {
 // The photon map of photon_list: built on the device (photon_build.hip) unless it fits one
 // leaf or DISTRAYTRACER_PHOTON_BUILD=host asks for the host build (csrc/photon.cpp; the two
 // are identical -- a GPU test checks it).
-static int set_photon_map(rt_scene* s, std::vector<double>& pos, std::vector<double>& pwr) {
+int rt::set_photon_map(rt_scene* s, std::vector<double>& pos, std::vector<double>& pwr) {
   HostScene& h = s->hs;
   const int64_t n = (int64_t)(pos.size() / 3);
   const char* mode = std::getenv("DISTRAYTRACER_PHOTON_BUILD");

@@ -54,7 +54,11 @@ EXPORTS = ["rt_abi_version", "rt_build_id", "rt_last_error", "rt_device_count", 
            "rt_render_variant", "rt_rank_plan", "rt_group_unique_id", "rt_group_create", "rt_group_create_rank", "rt_group_render",
            "rt_group_sync", "rt_group_render_host", "rt_group_frame", "rt_group_info", "rt_group_plan",
            "rt_group_rank_pixels", "rt_group_kernel_ms", "rt_group_time_rank", "rt_group_count", "rt_group_rebalance",
-           "rt_group_destroy", "rt_group_rccl_selftest"]
+           "rt_group_destroy", "rt_group_rccl_selftest",
+           # ABI 7: communicators (RCCL / caller host transport), the group and the photon pre-pass over them
+           "rt_comm_create_rccl", "rt_comm_create_host", "rt_comm_info", "rt_comm_destroy", "rt_comm_selftest",
+           "rt_group_create_comm",
+           "rt_photons_build_comm", "rt_photons_build_local"]
 
 _lib = None
 
@@ -149,6 +153,18 @@ def lib():
             L.rt_group_destroy.argtypes = [vp]
             L.rt_group_destroy.restype = None
             L.rt_group_rccl_selftest.argtypes = [i32, i32]
+        if hasattr(L, "rt_comm_create_host"):  # ABI >= 7
+            vp, i32, dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+            L.rt_comm_create_rccl.argtypes = [i32, i32, vp, i32, ctypes.POINTER(vp)]
+            L.rt_comm_create_host.argtypes = [i32, i32, ctypes.POINTER(CommOps), ctypes.POINTER(vp)]
+            L.rt_comm_info.argtypes = [vp, vp, i32]
+            L.rt_comm_destroy.argtypes = [vp]
+            L.rt_comm_destroy.restype = None
+            L.rt_comm_selftest.argtypes = [vp, i32]
+            L.rt_group_create_comm.argtypes = [vp, vp, ctypes.POINTER(RenderParams), ctypes.c_uint32, dbl, i32,
+                                               ctypes.POINTER(vp)]
+            L.rt_photons_build_comm.argtypes = [vp, vp, ctypes.c_uint64]
+            L.rt_photons_build_local.argtypes = [vp, i32, ctypes.c_uint64]
         _lib = L
     return _lib
 
@@ -201,6 +217,8 @@ def rank_plan(cost, world: int, heavy: float = 0.0, slots: int = 0, weight=None)
     weight: per-tile cut factors (the runs hold equal sums of cost x weight)."""
     c = np.ascontiguousarray(cost, dtype=np.uint32)
     w = None if weight is None else np.ascontiguousarray(weight, dtype=np.float64)
+    if w is not None and w.shape != c.shape:  # the C side reads weight[t] for every tile
+        raise ValueError(f"rank_plan: weight has {w.size} entries, cost {c.size}")
     owner = np.zeros(len(c), dtype=np.int32)
     order = np.zeros(len(c), dtype=np.int32)
     _check(lib().rt_rank_plan(c.ctypes.data, None if w is None else w.ctypes.data, len(c), world, heavy, slots,
@@ -225,7 +243,124 @@ def rccl_selftest(device: int = 0, n: int = 4099) -> None:
 
 GROUP_RGB = 1  # RT_GROUP_RGB: exchange the float-RGB plane too
 GROUP_COPY = 2  # RT_GROUP_COPY: device copies in one process (ranks may share a device)
-GROUP_INFO = ["world", "local_ranks", "first_rank", "ntiles", "tiles_x", "tw", "th", "rccl", "frames"]
+GROUP_INFO = ["world", "local_ranks", "first_rank", "ntiles", "tiles_x", "tw", "th", "rccl", "frames", "plan_checks"]
+TRANSPORT_NAMES = {0: "copy", 1: "rccl", 2: "host"}
+
+# rt_comm_ops (include/distraytracer.h): the host transport's four blocking callbacks
+_BCAST = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int)
+_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+_SEND = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int)
+_RECV = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int)
+
+
+class CommOps(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("bcast", _BCAST), ("allgather", _ALLGATHER), ("send", _SEND),
+                ("recv", _RECV)]
+
+
+def _host_bytes(addr: int, n: int):
+    """A writable uint8 torch view of n host bytes at addr (no copy)."""
+    import torch
+
+    return torch.frombuffer((ctypes.c_uint8 * n).from_address(addr), dtype=torch.uint8)
+
+
+class Comm:
+    """A communicator (rt_comm_*): RCCL (`rccl`) or the host transport (`host`) whose collectives
+    are torch.distributed calls on CPU tensors (gloo) -- the caller's-own-transport path, which lets
+    the ranks of one-process-per-GPU groups share a device."""
+
+    def __init__(self, handle, keep=None):
+        self._h = handle
+        self._keep = keep  # the callbacks (ctypes must keep them alive while the library may call them)
+
+    @classmethod
+    def rccl(cls, rank: int, world: int, uid, device: int) -> "Comm":
+        h = ctypes.c_void_p()
+        u = ctypes.create_string_buffer(bytes(uid), 128) if uid is not None else None
+        _check(lib().rt_comm_create_rccl(rank, world, u, device, ctypes.byref(h)), "rt_comm_create_rccl")
+        return cls(h)
+
+    @classmethod
+    def host(cls, dist, group=None) -> "Comm":
+        """Host transport over an initialised torch.distributed process group (gloo: CPU tensors)."""
+        import torch
+
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        errors = []
+
+        def guard(fn):
+            def call(*a):
+                try:
+                    fn(*a)
+                    return 0
+                except Exception as e:  # reported as RT_E_HIP by the library; the message kept here
+                    errors.append(repr(e))
+                    return 1
+            return call
+
+        def bcast(_ctx, buf, n, root):
+            dist.broadcast(_host_bytes(buf, n), root, group=group)
+
+        def allgather(_ctx, inp, out, n):
+            src = _host_bytes(inp, n).clone()
+            outs = [torch.empty(n, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(outs, src, group=group)
+            _host_bytes(out, n * world).copy_(torch.cat(outs))
+
+        def send(_ctx, buf, n, peer):
+            dist.send(_host_bytes(buf, n).clone(), peer, group=group)
+
+        def recv(_ctx, buf, n, peer):
+            t = torch.empty(n, dtype=torch.uint8)
+            dist.recv(t, peer, group=group)
+            _host_bytes(buf, n).copy_(t)
+
+        cbs = (_BCAST(guard(bcast)), _ALLGATHER(guard(allgather)), _SEND(guard(send)), _RECV(guard(recv)))
+        ops = CommOps(None, *cbs)
+        h = ctypes.c_void_p()
+        _check(lib().rt_comm_create_host(rank, world, ctypes.byref(ops), ctypes.byref(h)), "rt_comm_create_host")
+        c = cls(h, (cbs, ops))
+        c.errors = errors
+        return c
+
+    def selftest(self, n: int = 1031):
+        """rt_comm_selftest: all-gather, a broadcast from every rank and (host transport) the group's
+        send / receive pattern, checked on the host (collective). Raises RTError on a failure."""
+        rc = lib().rt_comm_selftest(self._h, n)
+        if rc != 0:
+            extra = f" (callback errors: {self.errors})" if getattr(self, "errors", None) else ""
+            raise RTError(f"rt_comm_selftest failed ({rc}): {lib().rt_last_error().decode()}{extra}")
+
+    def info(self) -> dict:
+        v = np.zeros(4, dtype=np.int64)
+        _check(lib().rt_comm_info(self._h, v.ctypes.data, 4), "rt_comm_info")
+        return {"rank": int(v[0]), "world": int(v[1]), "transport": TRANSPORT_NAMES.get(int(v[2]), "?"),
+                "device": int(v[3])}
+
+    def close(self):
+        if self._h:
+            lib().rt_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def build_photons_local(scenes, seed: int):
+    """rt_photons_build_local: the sharded photon pre-pass emulated in one process (scene q shoots
+    shard q of len(scenes); scenes may repeat); every distinct scene gets the merged map."""
+    arr = (ctypes.c_void_p * len(scenes))(*[s._h for s in scenes])
+    _check(lib().rt_photons_build_local(arr, len(scenes), seed), "rt_photons_build_local")
 
 
 class Group:
@@ -246,6 +381,17 @@ class Group:
         _check(lib().rt_group_create(arr, len(scenes), ctypes.byref(p), gf, heavy, slots, ctypes.byref(h)),
                "rt_group_create")
         return cls(h, list(scenes))
+
+    @classmethod
+    def create_comm(cls, scene, comm, W, H, spp=0, seed=0x5EED0001, flags=0, rgb=False, heavy=0.0, slots=0):
+        """One rank of a one-process-per-GPU group over a communicator (rt_group_create_comm; collective).
+        comm None: a one-rank group."""
+        p = params(W, H, spp, seed, None, 1, flags, 1)
+        h = ctypes.c_void_p()
+        _check(lib().rt_group_create_comm(scene._h, comm._h if comm is not None else None, ctypes.byref(p),
+                                          GROUP_RGB if rgb else 0, heavy, slots, ctypes.byref(h)),
+               "rt_group_create_comm")
+        return cls(h, [scene, comm])
 
     @classmethod
     def create_rank(cls, scene, rank, world, uid, W, H, spp=0, seed=0x5EED0001, flags=0, rgb=False, heavy=0.0,
@@ -423,6 +569,11 @@ class Scene:
 
     def build_photons(self, seed: int):
         _check(lib().rt_photons_build(self._h, seed), "rt_photons_build")
+
+    def build_photons_comm(self, comm, seed: int):
+        """The photon pre-pass sharded over a communicator's ranks (rt_photons_build_comm; collective)."""
+        _check(lib().rt_photons_build_comm(self._h, comm._h if comm is not None else None, seed),
+               "rt_photons_build_comm")
 
     def shoot_photons(self, seed: int, first: int, count: int):
         """Photon shard [first, first+count) of every light -> (pos, pwr, per_light counts)."""

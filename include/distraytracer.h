@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 enum rt_status {
   RT_OK = 0,
@@ -334,7 +334,8 @@ typedef struct rt_group rt_group;
    bucket, row-major inside a bucket): a rank's run and split tiles are the subsequences of order it
    owns. heavy <= 0: 1.25 (a tile is split when its cost exceeds heavy x total / (slots x world));
    slots <= 0: 4096 (wave slots of one MI355X at the render kernel's occupancy). weight (may be NULL):
-   per-tile factors of the cut (the runs hold equal sums of cost x weight; rt_group_rebalance). */
+   per-tile factors of the cut (the runs hold equal sums of cost x weight; rt_group_rebalance); it must
+   hold ntiles entries, like cost. */
 int rt_rank_plan(const uint32_t* cost, const double* weight, int ntiles, int world, double heavy, int slots,
                  int32_t* owner, int32_t* order);
 /* One process, n ranks: scenes[i] (rt_scene_create / rt_scene_load_cli on its device) is rank i.
@@ -344,7 +345,8 @@ int rt_group_create(rt_scene* const* scenes, int n, const rt_render_params* p, u
                     rt_group** out);
 /* One process per GPU: this process is `rank` of `world` (collective: every rank calls it). unique_id:
    the 128 bytes rt_group_unique_id returned on rank 0, shared by the caller (e.g. over
-   torch.distributed); rank 0 calibrates and broadcasts the tile costs over RCCL. */
+   torch.distributed); rank 0 calibrates and broadcasts the tile costs over RCCL. The group makes and
+   owns an RCCL communicator (rt_comm_create_rccl + rt_group_create_comm). */
 int rt_group_unique_id(void* id, int cap);
 int rt_group_create_rank(rt_scene* scene, int rank, int world, const void* unique_id, const rt_render_params* p,
                          uint32_t flags, double heavy, int slots, rt_group** out);
@@ -357,8 +359,9 @@ int rt_group_sync(rt_group* g);
    draw() over N GPUs; other processes render their part and return. */
 int rt_group_render_host(rt_group* g, float* rgb, int32_t* argb);
 int rt_group_frame(rt_group* g, float** d_rgb, int32_t** d_argb);
-/* info[0..8]: world, ranks driven by this process, first of them, layout tiles, tiles_x, tw, th,
-   transport (1 RCCL / 0 copies), frames enqueued */
+/* info[0..9]: world, ranks driven by this process, first of them, layout tiles, tiles_x, tw, th,
+   transport (1 RCCL / 2 host comm / 0 copies or one rank), frames enqueued, plan checks passed
+   (rank mode, world > 1: the collective plan agreement checks, one per cut) */
 int rt_group_info(const rt_group* g, int64_t* info, int n);
 /* the plan (rt_rank_plan's owner / order, up to cap tiles); returns the tile count */
 int rt_group_plan(const rt_group* g, int32_t* owner, int32_t* order, int cap);
@@ -383,6 +386,60 @@ int rt_group_count(rt_group* g, int rank, uint64_t* stats);
    after the last cut. */
 int rt_group_rebalance(rt_group* g, int rounds, int iters, double* rank_ms);
 void rt_group_destroy(rt_group* g);
+/* ---- Communicators (ABI 7) ------------------------------------------------------------------------
+   The transport a one-process-per-GPU group and the sharded photon pre-pass run their collectives
+   over. Two kinds:
+     RCCL  rt_comm_create_rccl: an RCCL communicator of `world` ranks (unique_id from
+           rt_group_unique_id on rank 0, shared by the caller); the frame exchange is stream-ordered
+           ncclSend / ncclRecv over xGMI. One device per rank (RCCL refuses two ranks on one device).
+     host  rt_comm_create_host: the caller's own transport (e.g. Java sockets / MPI, or
+           torch.distributed's gloo in the tests) as four blocking callbacks on HOST buffers; the frame
+           exchange stages the packed pixels through pinned host memory. Ranks may share a device, so
+           an N-rank frame runs as N processes on one GPU -- the same rank-mode code path as RCCL
+           (cost broadcast, plan check, receive offsets, rebalance all-gather), only the byte mover
+           differs.
+   Every collective of a group or of rt_photons_build_comm is entered by every rank in the same order
+   with the same sizes; a rank's local failure travels as a status word inside that collective, so
+   all ranks fail together instead of leaving peers blocked. A communicator must outlive the groups
+   made from it and is used by one thread at a time. */
+typedef struct rt_comm rt_comm;
+typedef struct rt_comm_ops {
+  void* ctx; /* passed back to every callback */
+  /* each returns 0 on success (nonzero: the calling rt_* function returns RT_E_HIP) */
+  int (*bcast)(void* ctx, void* buf, int64_t bytes, int root);               /* in place, from root */
+  int (*allgather)(void* ctx, const void* in, void* out, int64_t bytes);     /* out[world * bytes], rank order */
+  int (*send)(void* ctx, const void* buf, int64_t bytes, int peer);          /* blocking point-to-point */
+  int (*recv)(void* ctx, void* buf, int64_t bytes, int peer);
+} rt_comm_ops;
+int rt_comm_create_rccl(int rank, int world, const void* unique_id, int device, rt_comm** out);
+int rt_comm_create_host(int rank, int world, const rt_comm_ops* ops, rt_comm** out);
+/* info[0..3]: rank, world, transport (1 RCCL / 2 host), device (-1 for host) */
+int rt_comm_info(const rt_comm* comm, int64_t* info, int n);
+void rt_comm_destroy(rt_comm* comm);
+/* Diagnostics: the communicator's collectives on n int32 per rank, data checked on the host -- an
+   all-gather, a broadcast from every rank, and (host transport) the group's exchange pattern: ranks
+   > 0 send to rank 0 in rank order and rank 0 answers each. Collective; host-only for the host
+   transport (no GPU needed), so the transport's bindings are testable on a CPU. */
+int rt_comm_selftest(rt_comm* comm, int n);
+/* rt_group_create_rank over a communicator (collective: every rank calls it). Rank 0 calibrates the
+   layout and broadcasts the tile costs; before that the ranks check that they were given the same
+   frame (size, spp, seed, flags, heavy, slots), and after every cut (here and in rt_group_rebalance)
+   that they derived the same plan -- every sender's offset in rank 0's receive slab, pixel count and
+   pixel-list hash against rank 0's receive side (rt_group_info plan_checks counts the checks passed).
+   A NULL comm is a one-rank group. */
+int rt_group_create_comm(rt_scene* scene, rt_comm* comm, const rt_render_params* p, uint32_t flags, double heavy,
+                         int slots, rt_group** out);
+/* The photon pre-pass (myScene.initRender, myScene.java:1096-1099) sharded over a communicator's
+   ranks: rank r shoots emitted photons [r P / N, (r + 1) P / N) of every light
+   (sendDiffusePhotons / sendCausticPhotons, myScene.java:952-1091, same keyed RNG), the shards are
+   exchanged (each rank's records broadcast from it), merged into the reference's photon_list order
+   (light-major, then photon index, then path order) and every rank builds the same photon map: the
+   scene ends as rt_photons_build leaves it, bit for bit. Collective; NULL comm = rt_photons_build.
+   rt_photons_build_local: the same over n scenes in one process (scenes[q] shoots shard q; scenes
+   may repeat, e.g. n ranks emulated on one device); every distinct scene gets the merged map. */
+int rt_photons_build_comm(rt_scene* scene, rt_comm* comm, uint64_t seed);
+int rt_photons_build_local(rt_scene* const* scenes, int n, uint64_t seed);
+
 /* Diagnostics: every RCCL entry point the group resolves at run time, called on `device` through a
    one-rank communicator -- ncclCommInitRank and ncclCommInitAll, ncclBroadcast, ncclAllGather and a
    grouped ncclSend / ncclRecv to itself of n int32 -- with the data checked on the host. A one-GPU

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(rt.EXPORTS)
-    assert L.rt_abi_version() == 6
+    assert L.rt_abi_version() == 7
     # provenance: the library carries the build id of the sources and flags it was built from
     from distraytracer_old_amd import build
     assert rt.build_id() == build.built_id() == build.build_id()
@@ -128,3 +128,11 @@ def test_group_unique_id_loads_rccl():
     and hands out a 128-byte unique id without a GPU (ncclGetUniqueId needs none)."""
     u = rt.group_unique_id()
     assert len(u) == 128 and any(u)
+
+
+def test_rank_plan_rejects_a_short_weight_array():
+    """rt_rank_plan reads weight[t] for every tile: the binding refuses a weight array of another length."""
+    with pytest.raises(ValueError):
+        rt.rank_plan(np.ones(8, dtype=np.uint32), 2, weight=np.ones(5))
+    owner, order = rt.rank_plan(np.ones(8, dtype=np.uint32), 2, weight=np.ones(8))
+    assert sorted(order.tolist()) == list(range(8)) and 0 <= owner.min() and owner.max() < 4  # world + r: split tiles

@@ -160,3 +160,58 @@ def test_rccl_transport_bindings_on_one_device():
     what covers the bindings before the driver's multi-GPU run; the exchange logic itself is covered
     by the COPY-transport emulation above."""
     rt.rccl_selftest(0, 4099)
+
+
+@pytest.mark.parametrize("n", [1, 2, 8])
+def test_photons_build_local_equals_unsharded(n):
+    """rt_photons_build_local: the pre-pass sharded over n emulated ranks (each shoots its emitted-photon
+    range, merged light-major / index / path order) equals rt_photons_build bit for bit -- the
+    photon_list and the device map."""
+    cli, seed = "t11.cli", 0x5EED0005
+    ref = _scene(cli, seed)
+    g = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+    rt.build_photons_local([g] * n, seed)
+    p0, w0 = ref.photons()
+    p1, w1 = g.photons()
+    assert len(p0) > 0 and p0.shape == p1.shape
+    assert np.array_equal(p0.view(np.uint64), p1.view(np.uint64)) and np.array_equal(w0.view(np.uint64), w1.view(np.uint64))
+    assert rt.photon_maps_equal(g.photon_map(), ref.photon_map())
+    # the comm entry without a communicator is the unsharded build
+    h = rt.Scene.load_cli(cli, textures=scenes.prepare(cli))
+    h.build_photons_comm(None, seed)
+    assert rt.photon_maps_equal(h.photon_map(), ref.photon_map())
+
+
+def test_group_create_comm_one_rank_and_device_guard():
+    """rt_group_create_comm without a communicator is a one-rank group (same frame); the group's
+    entry points leave the caller's current device as they found it."""
+    import torch
+
+    cli, W, H, spp, seed = CASES[0]
+    g = _scene(cli)
+    rgb, argb = g.render(W, H, spp=spp, seed=seed)
+    with rt.Group.create_comm(g, None, W, H, spp=spp, seed=seed) as grp:
+        assert grp.info()["world"] == 1 and grp.info()["plan_checks"] == 0
+        _, a = grp.render_host(W, H, rgb=False)
+        assert np.array_equal(a, argb)
+        assert torch.cuda.current_device() == 0
+
+
+def test_group_rccl_two_devices_one_process():
+    """rt_group_create over 2 distinct devices (ncclCommInitAll; RCCL send / receive into rank 0's
+    slab): only where 2 GPUs are visible."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    cli, W, H, spp, seed = CASES[0]
+    g0 = rt.Scene.load_cli(cli, textures=scenes.prepare(cli), device=0)
+    g1 = rt.Scene.load_cli(cli, textures=scenes.prepare(cli), device=1)
+    rgb, argb = g0.render(W, H, spp=spp, seed=seed)
+    with rt.Group.create([g0, g1], W, H, spp=spp, seed=seed, rgb=True, heavy=0.1, slots=64) as grp:
+        assert grp.info()["rccl"] == 1
+        grp.rebalance(rounds=1, iters=2)
+        for _ in range(2):
+            c, a = grp.render_host(W, H)
+            assert np.array_equal(a, argb)
+            assert np.array_equal(c.view(np.uint32), rgb.view(np.uint32))
