@@ -28,8 +28,10 @@ reported beside it. traffic: measured HBM bytes per launch (FETCH_SIZE x 2 + WRI
 from the newest committed rocprofv3 --pmc summary of the workload in profiles/ when it is of
 this library build (rt_build_id) and its kernel time is within 5 % of this run's, else null
 (traffic_missing says why); fp64: the kernel's fp64 FLOP rate (same PMC summary) against the measured fp64
-VALU peak (tools/fp64_peak.hip); valu: the share of the SIMDs' VALU issue slots the kernel fills (same
-PMC summary) -- the bound this branchy fp64 traversal runs into.
+VALU peak (tools/fp64_peak.hip); valu: the share of the SIMDs' VALU issue slots the kernel fills at an
+assumed 4 cycles per instruction; valu_measured: the same from MEASURED issue costs per instruction
+class (tools/valu_issue.hip x the PMC class counts, tools/valu_model.py) -- the bound this branchy
+fp64 traversal runs into.
 
 cpu_baseline: the oracle (CPU restatement of the reference path, fp64) timed on
 the box's CPU share (affinity / cgroup quota / OMP_NUM_THREADS; the host's CPU count and model
@@ -114,6 +116,51 @@ def find_pmc(workload: str, build_id: str, kern_ms: float):
             return d, Path(f).name, None
         break  # only the newest summary of the workload is a candidate
     return None, None, why
+
+
+# PMC instruction classes of the VALU issue model (tools/valu_model.py cost_ns keys)
+VALU_CLASSES = {"add_f64": "SQ_INSTS_VALU_ADD_F64", "mul_f64": "SQ_INSTS_VALU_MUL_F64", "fma_f64": "SQ_INSTS_VALU_FMA_F64",
+                "trans_f64": "SQ_INSTS_VALU_TRANS_F64", "add_f32": "SQ_INSTS_VALU_ADD_F32",
+                "mul_f32": "SQ_INSTS_VALU_MUL_F32", "fma_f32": "SQ_INSTS_VALU_FMA_F32",
+                "trans_f32": "SQ_INSTS_VALU_TRANS_F32", "int32": "SQ_INSTS_VALU_INT32",
+                "int64": "SQ_INSTS_VALU_INT64", "cvt": "SQ_INSTS_VALU_CVT"}
+
+
+def find_valu_model(variant: int):
+    """The newest committed VALU issue model (profiles/*valu_model*.json, tools/valu_model.py) of this
+    render-kernel variant: measured issue cost per instruction class."""
+    for f in sorted(glob.glob(str(REPO / "profiles" / "*valu_model*.json")), reverse=True):
+        try:
+            d = json.loads(Path(f).read_text())
+        except Exception:
+            continue
+        if d.get("variant_F") == variant and d.get("cost_ns"):
+            return d, Path(f).name
+    return None, None
+
+
+def valu_issue(cnt: dict, vm: dict, n_simd: int, kern_ms: float):
+    """Share of the SIMDs' VALU issue capacity the kernel's instructions fill: sum over PMC classes of
+    count x measured cost (tools/valu_issue.hip: ns per wave instruction per SIMD at saturation), the
+    unclassified rest at its static-mix cost, over SIMDs x kernel time. None without the class counts."""
+    cost = vm["cost_ns"]
+    if not all(c in cnt for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                  "SQ_INSTS_VALU_INT32")):
+        return None
+    total = float(cnt["SQ_INSTS_VALU"])
+    per, known = {}, 0.0
+    for k, c in VALU_CLASSES.items():
+        if c in cnt:
+            per[k] = float(cnt[c]) * cost[k]
+            known += float(cnt[c])
+    per["rest"] = max(0.0, total - known) * cost["rest"]
+    avail = n_simd * kern_ms * 1e6  # SIMD-ns
+    return {"issue_frac": sum(per.values()) / avail,
+            "by_class": {k: v / avail for k, v in per.items()},
+            "classes_counted": sorted(k for k in VALU_CLASSES if VALU_CLASSES[k] in cnt),
+            "note": "sum of PMC class counts x measured saturated issue cost per wave instruction "
+                    "(tools/valu_issue.hip, 8 waves / SIMD); the unclassified rest (moves, compares, "
+                    "selects, lane ops) at the mean cost of its static in-loop mix (tools/valu_model.py)"}
 
 
 def cpu_share() -> dict:
@@ -439,7 +486,7 @@ def main():
         bid = rt.build_id()
         pmc, tsrc, why = find_pmc(workload, bid, kern_ms) if world == 1 else (None, None, "N > 1")
         traffic = traffic_rd = traffic_wr = traffic_lo = None
-        fp64 = valu = None
+        fp64 = valu = valu_measured = None
         if pmc:
             traffic_rd = float(pmc["hbm_bytes_per_launch"])
             traffic_wr = pmc.get("hbm_write_bytes_per_launch")
@@ -451,6 +498,12 @@ def main():
                         "flop_per_launch": float(pmc["fp64_flop_per_launch"]),
                         "note": "fp64 VALU wave instructions x 64 lanes (inactive lanes included: an upper bound)"}
             cnt = pmc.get("counters") or {}
+            vm, vm_src = find_valu_model(var_t)
+            if cnt.get("SQ_INSTS_VALU") and vm:
+                valu_measured = valu_issue(cnt, vm, 4 * torch.cuda.get_device_properties(dev).multi_processor_count,
+                                           kern_ms)
+                if valu_measured:
+                    valu_measured["model"] = vm_src
             if cnt.get("SQ_INSTS_VALU"):
                 # the bound this fp64 traversal actually runs into: the SIMDs' VALU issue. A wave64 VALU
                 # instruction occupies a 16-lane SIMD for 4 cycles (the fp64 FMA rate the peak is quoted on)
@@ -524,7 +577,7 @@ def main():
                          # ... and the same per-lane accounting of the work the kernel does (culling on)
                          "cache_served_gbps_8d_per_lane_executed": achieved_lane_x,
                          "bytes_per_ray_8d_per_lane_executed": xbytes_frame / max(1.0, rays_frame),
-                         "fp64": fp64, "valu": valu},
+                         "fp64": fp64, "valu": valu, "valu_measured": valu_measured},
         }
         if world > 1 and args.backend == "gloo":
             out["rehearsal"] = f"gloo backend, {world} ranks on {ndev} GPU(s): not a scaling measurement"

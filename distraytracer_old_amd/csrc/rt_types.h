@@ -65,6 +65,15 @@ struct NodeD {
                     // = the right child's fat-edge bound
 };
 static_assert(sizeof(NodeD) == 128, "NodeD is two 64-B lines");
+// fp32 copy of a NodeD's child boxes for the conservative fp32 box pre-test of the packet traversals
+// (trace_kernels.h box32): b = left min[3] max[3], right min[3] max[3] rounded to nearest; mag >= every
+// |coordinate| of both boxes; sl / sr >= the children's fat-edge bounds (node_slack) -- +inf where a
+// value does not fit a float (the pre-test then settles nothing and the fp64 tests decide)
+struct NodeF {
+  float b[12];
+  float mag, sl, sr, pad;
+};
+static_assert(sizeof(NodeF) == 64, "NodeF is one 64-B line");
 struct LeafD {
   int32_t start, count;  // range in leaf member refs (>= 0 tri index, < 0 ~prim index)
 };
@@ -153,6 +162,7 @@ struct SceneD {
   const double* triUV;  // [ntri][3][2] texture_coord, nullptr when no triangle is image-textured
   const PrimD* prim;
   const NodeD* node;
+  const NodeF* nodeF;   // [nnode] fp32 boxes of the BVH nodes (box32)
   const LeafD* leaf;
   const int32_t* member;
   const AccelD* accel;

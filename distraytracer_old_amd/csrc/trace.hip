@@ -250,6 +250,30 @@ static int upload_scene(rt_scene* s) {
       (rc = upload(s, h.accel, &d.accel)) || (rc = upload(s, h.top, &d.top)) || (rc = upload(s, h.mat, &d.mat)) ||
       (rc = upload(s, h.light, &d.light)) || (rc = upload(s, h.tex, &d.tex)) || (rc = upload(s, h.texel, &d.texel)))
     return rc;
+  {  // fp32 node boxes (trace_kernels.h box32): coordinates rounded to nearest, bounds rounded up
+    auto f32 = [](double x) { return std::fabs(x) <= 3.0e38 ? (float)x : (x < 0 ? -INFINITY : INFINITY); };
+    auto f32_up = [](double x) {  // >= x >= 0 (inf when it does not fit)
+      const double u = x * (1 + 0x1p-20);
+      return (u >= 0 && u <= 3.0e38) ? (float)u : INFINITY;
+    };
+    std::vector<NodeF> nf(h.node.size());
+    for (size_t i = 0; i < h.node.size(); ++i) {
+      NodeD& n = h.node[i];
+      const double* src[4] = {n.lmin, n.lmax, n.rmin, n.rmax};
+      double mag = 0;
+      for (int q = 0; q < 4; ++q)
+        for (int c = 0; c < 3; ++c) {
+          nf[i].b[3 * q + c] = f32(src[q][c]);
+          mag = std::max(mag, std::fabs(src[q][c]));
+        }
+      nf[i].mag = std::isfinite(mag) ? f32_up(mag) : INFINITY;
+      const double sl = node_slack(n, 0), sr = node_slack(n, 1);  // set for nearest-first accels only
+      nf[i].sl = std::isfinite(sl) && sl >= 0 ? f32_up(sl) : INFINITY;
+      nf[i].sr = std::isfinite(sr) && sr >= 0 ? f32_up(sr) : INFINITY;
+      nf[i].pad = 0;
+    }
+    if ((rc = upload(s, nf, &d.nodeF))) return rc;
+  }
   d.triUV = nullptr;
   {  // triangle UVs only matter for image-textured triangles
     bool need = false;

@@ -466,6 +466,18 @@ DEVI lds_u64* pkM() { return (lds_u64*)(pkB() + PKO_M); }
 enum { SL_BASE = 0, SL_LTM = 3, SL_TEX = 4, SL_NRM = 7, SL_DW = 10, SL_RGB = 13, SL_N = 16, SL_RAYO = 0, SL_RAYD = 3,
        SL_KEY = 3, SL_FWD = 13 };
 DEVI void stash(int q, double v) { pkT()[q * 64 + __lane_id()] = v; }
+// A wave-uniform value (kernel argument, in SGPRs) made opaque where it is used: what is derived
+// from it (its copy into VGPRs, a conversion) is then computed at the use instead of being hoisted
+// out of the sample loop and spilled to scratch across the shading tree -- a per-wave store of 64
+// copies of the same value (RT_UNI_OPAQUE; C3 wrote ~4 KB per wave that way at the loop's entry)
+#ifndef RT_UNI_OPAQUE
+#define RT_UNI_OPAQUE 1
+#endif
+template <class T>
+DEVI T uni_here(T v) {
+  if (RT_UNI_OPAQUE) asm volatile("" : "+s"(v));
+  return v;
+}
 DEVI double unstash(int q) { return pkT()[q * 64 + __lane_id()]; }
 DEVI void stash3(int q, V v) { stash(q, v.x); stash(q + 1, v.y); stash(q + 2, v.z); }
 DEVI V unstash3(int q) { return mk(unstash(q), unstash(q + 1), unstash(q + 2)); }
@@ -640,6 +652,77 @@ DEVI bool nf_child(const ChildBox& c, double s, double ymax, V o, V d, const Ray
   e = entry_grown(c.mn, c.mx, s, o, ri.y);
   return e <= lim;
 }
+// ---- conservative fp32 box pre-test (RT_F32_BOX) ---------------------------------------------
+// The packet traversals' child-box tests first run in fp32 on the node's fp32 boxes (NodeF): a
+// wave64 f32 fma / add / min is issued at twice the rate of its fp64 form on gfx950, and the whole
+// test is ~22 instructions instead of ~30 fp64 ones (tools/valu_issue.hip). A decision
+// is taken from fp32 only when it is certain, and then it is the reference's (myBBox.intersectCheck,
+// myGeomBase.java:132-162); every other lane runs the existing fp64 tests. The bound: with
+// t = (b - o) y (real, y the fp64 reciprocal), the fp32 slab value t' = fma(RN(b), RN(y), RN(-RN(o) RN(y)))
+// satisfies |t' - t| <= 2^-21 |y| (|b| + |o|) (four roundings of 2^-24, |t| <= |y| (|b| + |o|)), so with
+// E = 2^-20 ymax (mag + omax) (mag >= |b| over the node's two boxes, both bounds rounded up) the fp32
+// entry / exit lo', hi' are within E of the real ones, and each fp32 compare below rounds by at most
+// 2^-24 of values <= 2^20 E: a miss is certain when hi' < lo' - 4E or lo' < -2E, a hit when
+// hi' > lo' + 4E and lo' > 2E (the reference's own rounding, ~2^-51 relative, is far inside these
+// margins). Overflow makes E (and the test) +inf or NaN: nothing is settled then.
+#ifndef RT_F32_BOX
+#define RT_F32_BOX 1
+#endif
+// In the shadow (any-hit) packet traversal it pays in the transparent variants (C4 484 -> 455 ms, C5
+// 175.1 -> 173.4 ms) but not in C3's triangles-only variant, whose shading code then spills (2.90 ->
+// 2.96 ms); the nearest-first closest hit gains in C3 (2.94 -> 2.90 ms). Same images
+// (profiles/r06f_f32_ab.log).
+#ifndef RT_F32_SHADOW  // the fp32 pre-test in the shadow (any-hit) packet traversal
+#define RT_F32_SHADOW 1
+#endif
+#ifndef RT_F32_SHADOW_TRANS  // ... of the transparent variants
+#define RT_F32_SHADOW_TRANS 1
+#endif
+#ifndef RT_F32_SHADOW_OPAQUE  // ... of the other variants
+#define RT_F32_SHADOW_OPAQUE 0
+#endif
+struct RayF {
+  float y[3], noy[3];  // RN(y_i), RN(-RN(o_i) RN(y_i))
+  float ymax, omax;    // >= max |y_i|, >= max |o_i|
+};
+DEVI RayF ray_f32(V o, const RayInv& ri, double ymax) {
+  RayF r;
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  r.y[0] = (float)ri.y[0]; r.y[1] = (float)ri.y[1]; r.y[2] = (float)ri.y[2];
+  r.noy[0] = -(ox * r.y[0]); r.noy[1] = -(oy * r.y[1]); r.noy[2] = -(oz * r.y[2]);
+  r.ymax = (float)(ymax * (1 + 0x1p-20));
+  r.omax = (float)(fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z)) * (1 + 0x1p-20));
+  return r;
+}
+DEVI float f32_margin(const RayF& r, float mag) { return 0x1p-20f * (r.ymax * (mag + r.omax)); }
+enum : int { B32_MISS = 0, B32_HIT = 1, B32_OPEN = 2 };
+// b: min[3] max[3] of one child (fp32); lo: the fp32 entry (a settled hit's entry within E)
+DEVI int box32(const float* b, const RayF& r, float E, float& lo) {
+  const float t0 = __builtin_fmaf(b[0], r.y[0], r.noy[0]), t3 = __builtin_fmaf(b[3], r.y[0], r.noy[0]);
+  const float t1 = __builtin_fmaf(b[1], r.y[1], r.noy[1]), t4 = __builtin_fmaf(b[4], r.y[1], r.noy[1]);
+  const float t2 = __builtin_fmaf(b[2], r.y[2], r.noy[2]), t5 = __builtin_fmaf(b[5], r.y[2], r.noy[2]);
+  lo = fmaxf(fmaxf(fminf(t0, t3), fminf(t1, t4)), fminf(t2, t5));
+  const float hi = fminf(fminf(fmaxf(t0, t3), fmaxf(t1, t4)), fmaxf(t2, t5));
+  if (hi < lo - 4 * E || lo < -2 * E) return B32_MISS;
+  if (hi > lo + 4 * E && lo > 2 * E) return B32_HIT;
+  return B32_OPEN;
+}
+// nf_child's lower bound of a settled hit's grown entry: lo_real - s ymax >= (lo' - E) - s ymax, and
+// the two fp32 roundings here are covered by the further 2E and by s, ymax being rounded up
+DEVI double lb32(float lo, float E, float s, const RayF& r) { return (double)((lo - 3 * E) - s * r.ymax); }
+struct NodeBoxF {  // a node's fp32 record, scalar-loaded
+  float b[12];
+  float mag, sl, sr;
+};
+DEVI NodeBoxF sload_nodef(const NodeF* p) {
+  NodeBoxF n;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) n.b[i] = sload(p->b + i);
+  n.mag = sload(&p->mag); n.sl = sload(&p->sl); n.sr = sload(&p->sr);
+  return n;
+}
+DEVI int32_t sload_ref(const NodeD* nd, int side) { return sload(side ? &nd->right : &nd->left); }
+
 // a candidate t worth the inside test: it can beat (or, by leaf order, tie) this accel's best
 // and beats the best of the entries before it (their ties win: TreeMap keeps the first)
 struct LimNF {
@@ -656,6 +739,8 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
   int sp = 0;
   int32_t N = uni(A.root);
   const double ymax = fmax(fmax(fabs(ri.y[0]), fabs(ri.y[1])), fabs(ri.y[2]));  // RT_NF_LB
+  const bool f32 = RT_F32_BOX && RT_NF_LB && RT_NF_CODE && ri.fast;
+  const RayF rf = ray_f32(ao, ri, ymax);
 #if RT_NF_CODE
   int32_t curCode = 0;    // the child being entered (node << 1 | side): its box is reloaded for the inside test
 #else
@@ -664,6 +749,41 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
   while (true) {
     if (N >= 0) {  // internal: both children tested now, the nearer one entered, the other pushed
       const NodeD* nd = S.node + N;
+#if RT_F32_BOX && RT_NF_LB && RT_NF_CODE
+      // the fp32 pre-test on the node's 64-B fp32 record; the fp64 boxes are loaded only when a lane
+      // is left unsettled (grazing rays, or a ray the pre-test cannot bound)
+      const NodeBoxF nb = sload_nodef(S.nodeF + N);
+      struct { int32_t ref; } cl{sload_ref(nd, 0)}, cr{sload_ref(nd, 1)};
+      WCNT(C_WNODE, 1);  // a node visit (8(d) prices one at 64 B, as the reference order's)
+      bool hl = false, hr = false, ol = false, orr = false;
+      double el = DMAX, er = DMAX;
+      const double bnd = fmin(best.t, bt), lim = fmin(bnd + bnd * 0x1p-40, 0x1p1000);  // a miss (DMAX) never passes
+      if (in_mask_t<MASKOPS<F>>(act)) {
+        if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }
+        if (f32) {
+          const float E = f32_margin(rf, nb.mag);
+          float lo;
+          const int cl32 = box32(nb.b, rf, E, lo);
+          if (cl32 == B32_HIT) { el = lb32(lo, E, nb.sl, rf); hl = el <= lim; if (!hl) el = DMAX; }
+          ol = cl32 == B32_OPEN;
+          const int cr32 = box32(nb.b + 6, rf, E, lo);
+          if (cr32 == B32_HIT) { er = lb32(lo, E, nb.sr, rf); hr = er <= lim; if (!hr) er = DMAX; }
+          orr = cr32 == B32_OPEN;
+        } else {
+          ol = orr = true;
+        }
+      }
+      if (__ballot(ol || orr)) {  // unsettled lanes: the fp64 tests (nf_child)
+        if (__ballot(ol)) {
+          const ChildBox c = sload_child(nd, 0);
+          if (ol) hl = nf_child<MASKOPS<F>>(c, sload_slack(nd, 0), ymax, ao, ad, ri, lim, el);
+        }
+        if (__ballot(orr)) {
+          const ChildBox c = sload_child(nd, 1);
+          if (orr) hr = nf_child<MASKOPS<F>>(c, sload_slack(nd, 1), ymax, ao, ad, ri, lim, er);
+        }
+      }
+#else
       const ChildBox cl = sload_child(nd, 0), cr = sload_child(nd, 1);
       const double sl = sload_slack(nd, 0), sr = sload_slack(nd, 1);
       WCNT(C_WNODE, 1);  // a node visit (8(d) prices one at 64 B, as the reference order's)
@@ -682,6 +802,7 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
           if (er <= lim) hr = box_hit<MASKOPS<F>>(cr.mn, cr.mx, ao, ad, ri);
         }
       }
+#endif
       const uint64_t L = __ballot(hl), R = __ballot(hr);
       if (L && R) {
         const int fl = (int)__builtin_ctzll(L & R);
@@ -746,19 +867,24 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
       --sp;
       const int32_t code = uni(pkN()[sp]);
       uint64_t M = uni64(pkM()[sp]);
-      const ChildBox cb = sload_child(S.node + (code >> 1), code & 1);
+      const NodeD* pn = S.node + (code >> 1);
       bool keep = false;
       if (in_mask_t<MASKOPS<F>>(M)) {
         const double bnd = fmin(best.t, bt), lim = fmin(bnd + bnd * 0x1p-40, 0x1p1000);  // a miss (DMAX) never passes
-        const double e = sp < PK_LDS ? pkT()[sp * 64 + __lane_id()]
-                                     : entry_grown(cb.mn, cb.mx, sload_slack(S.node + (code >> 1), code & 1), ao, ri.y);
+        double e;
+        if (sp < PK_LDS) {
+          e = pkT()[sp * 64 + __lane_id()];
+        } else {
+          const ChildBox cb = sload_child(pn, code & 1);
+          e = entry_grown(cb.mn, cb.mx, sload_slack(pn, code & 1), ao, ri.y);
+        }
         keep = e <= lim;
       }
       M = __ballot(keep);
 #if RT_NF_CODE
-      if (M) { curCode = code; act = M; N = cb.ref; break; }
+      if (M) { curCode = code; act = M; N = sload_ref(pn, code & 1); break; }
 #else
-      if (M) { cur = cb; act = M; N = cb.ref; break; }
+      if (M) { cur = sload_child(pn, code & 1); act = M; N = cur.ref; break; }
 #endif
     }
     if (N == INT32_MAX) break;
@@ -1101,6 +1227,18 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
   const RayInv ri = ray_inv(ao, ad, S.fastSlab & SCENE_FAST_SLAB);
   // (C3's triangles-only variant gains 2 %; the transparent variants lose as much: not there)
   const bool nearf = RT_ANY_NEAR && (RT_AN_TRANS || (F & FT_TRANS) == 0) && (S.fastSlab & SCENE_NEAREST_FIRST) && !__ballot(!w.stable);
+  // the fp32 box pre-test (box32): a shadow box decision -- hit and (dist - entry) - EPS > 0 -- is
+  // settled when the entry is certain to lie clear of dist - EPS (bracketed here by 2^-20 of it)
+  constexpr bool F32 = RT_F32_BOX && RT_F32_SHADOW && ((F & FT_TRANS) != 0 ? RT_F32_SHADOW_TRANS : RT_F32_SHADOW_OPAQUE);
+  const bool f32 = F32 && ri.fast;
+  RayF rf;
+  float dLo = 0, dHi = 0;
+  if constexpr (F32) {
+    rf = ray_f32(ao, ri, fmax(fmax(fabs(ri.y[0]), fabs(ri.y[1])), fabs(ri.y[2])));
+    const double dm = dist - EPS;
+    dLo = (float)(dm - fabs(dm) * 0x1p-20);
+    dHi = (float)(dm + fabs(dm) * 0x1p-20);
+  }
   PkStack st;
   int sp = 0;
   uint64_t act = __ballot(1);
@@ -1117,16 +1255,50 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
   }
   while (true) {
     if (N >= 0) {  // internal: push (right child pending), go left with the lanes whose left box is hit
-      const ChildBox cl = sload_child(S.node + N, 0);
-      const ChildBox cr = sload_child(S.node + N, 1);
       PKSTAT(P_AB_STEP, act);
       WCNT(C_WNODE, 1);
       bool hl = false, hr = false;
       double el = DMAX, er = DMAX;
-      if (in_mask_t<MASKOPS<F>>(act)) {
-        if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX]++; }
-        hl = box_shadow_e<MASKOPS<F>>(cl.mn, cl.mx, ao, ad, ri, dist, el);
-        hr = box_shadow_e<MASKOPS<F>>(cr.mn, cr.mx, ao, ad, ri, dist, er);
+      struct { int32_t ref; } cl{0}, cr{0};
+      if constexpr (F32) {
+        const NodeD* nd = S.node + N;
+        const NodeBoxF nb = sload_nodef(S.nodeF + N);
+        cl.ref = sload_ref(nd, 0);
+        cr.ref = sload_ref(nd, 1);
+        bool ol = false, orr = false;
+        if (in_mask_t<MASKOPS<F>>(act)) {
+          if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX]++; }
+          if (f32) {
+            const float E = f32_margin(rf, nb.mag);
+            float lo;
+            const int c0 = box32(nb.b, rf, E, lo);
+            if (c0 == B32_HIT && dLo > lo + 2 * E) { hl = true; el = lo; }
+            else ol = !(c0 == B32_MISS || dHi < lo - 2 * E);
+            const int c1 = box32(nb.b + 6, rf, E, lo);
+            if (c1 == B32_HIT && dLo > lo + 2 * E) { hr = true; er = lo; }
+            else orr = !(c1 == B32_MISS || dHi < lo - 2 * E);
+          } else {
+            ol = orr = true;
+          }
+        }
+        if (__ballot(ol)) {  // unsettled lanes: the fp64 test
+          const ChildBox c = sload_child(nd, 0);
+          if (ol) hl = box_shadow_e<MASKOPS<F>>(c.mn, c.mx, ao, ad, ri, dist, el);
+        }
+        if (__ballot(orr)) {
+          const ChildBox c = sload_child(nd, 1);
+          if (orr) hr = box_shadow_e<MASKOPS<F>>(c.mn, c.mx, ao, ad, ri, dist, er);
+        }
+      } else {
+        const ChildBox c0 = sload_child(S.node + N, 0);
+        const ChildBox c1 = sload_child(S.node + N, 1);
+        cl.ref = c0.ref;
+        cr.ref = c1.ref;
+        if (in_mask_t<MASKOPS<F>>(act)) {
+          if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX]++; }
+          hl = box_shadow_e<MASKOPS<F>>(c0.mn, c0.mx, ao, ad, ri, dist, el);
+          hr = box_shadow_e<MASKOPS<F>>(c1.mn, c1.mx, ao, ad, ri, dist, er);
+        }
       }
       const uint64_t R = __ballot(hr);
       const uint64_t H = __ballot(hl);
@@ -2391,7 +2563,7 @@ DEVI V background(const SceneD& S, const WRay& w, Counters& ct) {
       return texel(S, T, (long)jd2i(v) * T.w + jd2i(u));
     }
   }
-  return mk(S.bg[0], S.bg[1], S.bg[2]);
+  return mk(uni_here(S.bg[0]), uni_here(S.bg[1]), uni_here(S.bg[2]));
 }
 
 DEVI V rot_axis(V v1, V u, double thet) {  // rotVecAroundAxis (DistRayTracer.java:336-349)
@@ -3336,7 +3508,8 @@ DEVI PixGeo pix_geo(int lane, int tile, int tilesX, int ncols, const ParamsD& P)
   g.col = (F & FT_PASS) ? g.ci * P.colStep : g.ci;
   g.ri = ty * P.th + g.pl / P.tw;  // row index within this render's rows
   g.valid = g.ci < ncols && g.ri < P.nrows;
-  g.row = P.row0 + (g.ri / P.band) * P.rowStep * P.band + g.ri % P.band;
+  const int band = uni_here(P.band);  // (the division's reciprocal is not kept across the sample loop)
+  g.row = band == 1 ? P.row0 + g.ri * P.rowStep : P.row0 + (g.ri / band) * P.rowStep * band + g.ri % band;
   return g;
 }
 // the lane index as an opaque value: what is derived from it is recomputed where it is used
@@ -3423,8 +3596,8 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
     const PixGeo g = pix_geo<F>(opaque_lane(lane), tile, tilesX, ncols, P);
     const int j = g.j, pl = g.pl, col = g.col, row = g.row;
     const bool valid = g.valid;
-    const double rayY = (-1 * (row - P.H / 2.0));
-    const double rayX = col - P.W / 2.0;
+    const double rayY = (-1 * (row - uni_here(P.H) / 2.0));
+    const double rayX = col - uni_here(P.W) / 2.0;
     k.pixel = (uint64_t)row * (uint64_t)P.W + (uint64_t)col;
     const int s = s0 + j;
     V cc = mk(0, 0, 0);
@@ -3476,7 +3649,7 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
         double ry = rayY + rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_AA_Y, 0, -.5, .5);
         double rx = rayX + rng(P.seed, k.pixel, (uint32_t)s, 0, SITE_AA_X, 0, -.5, .5);
         o = mk(0, 0, 0);
-        d = mk(rx, ry, P.viewZ);
+        d = mk(rx, ry, uni_here(P.viewZ));
       }
       if (!SH_COMPACT && traced) {
         Key ks = k;

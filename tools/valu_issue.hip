@@ -24,14 +24,18 @@ constexpr int ITERS = 2048;
 enum Op {
   FMA_F64, ADD_F64, MUL_F64, MIN_F64, MAX_F64, CMP_F64_SGPR, CMP_F64_VCC, CNDMASK_B32, MOV_B32, MOV_B64,
   ADD_U32, LSHL_B32, AND_B32, LSHL_B64, ADD_CO_U32, MBCNT, READFIRSTLANE, DPP_MOV, ADD_F32, FMA_F32, MAX3_F32,
-  PK_ADD_F32, PK_FMA_F32, CVT_F32_F64, CMP_F32_SGPR, RCP_F64, FRACT_F64, NOP_OPS
+  PK_ADD_F32, PK_FMA_F32, CVT_F32_F64, CMP_F32_SGPR, RCP_F64, FRACT_F64,
+  CNDMASK_VCC, CMP_U32_VCC, CMP_CLASS_F64, OR_B32, LSHR_B32_VOP2, BFE_U32, MUL_LO_U32, CVT_F64_I32, LDEXP_F64,
+  WRITELANE, SUB_U32, MAX_I32, NOP_OPS
 };
 static const char* kNames[NOP_OPS] = {
     "v_fma_f64", "v_add_f64", "v_mul_f64", "v_min_f64", "v_max_f64", "v_cmp_lt_f64_e64(sgpr)",
     "v_cmp_lt_f64(vcc)", "v_cndmask_b32_e64", "v_mov_b32", "v_mov_b64", "v_add_u32", "v_lshlrev_b32",
     "v_and_b32", "v_lshlrev_b64", "v_add_co_u32", "v_mbcnt_lo_u32_b32", "v_readfirstlane_b32", "v_mov_b32_dpp",
     "v_add_f32", "v_fma_f32", "v_max3_f32", "v_pk_add_f32", "v_pk_fma_f32", "v_cvt_f32_f64",
-    "v_cmp_lt_f32_e64(sgpr)", "v_rcp_f64", "v_fract_f64"};
+    "v_cmp_lt_f32_e64(sgpr)", "v_rcp_f64", "v_fract_f64",
+    "v_cndmask_b32_e32(vcc)", "v_cmp_lt_u32(vcc)", "v_cmp_class_f64(vcc)", "v_or_b32", "v_lshrrev_b32(vgpr)",
+    "v_bfe_u32", "v_mul_lo_u32", "v_cvt_f64_i32", "v_ldexp_f64", "v_writelane_b32", "v_sub_u32", "v_max_i32"};
 
 template <int OP>
 __device__ __forceinline__ void body(double* d, uint32_t* u, uint64_t* m, float* f, double dy, double dz, uint32_t uy,
@@ -65,6 +69,18 @@ __device__ __forceinline__ void body(double* d, uint32_t* u, uint64_t* m, float*
     if constexpr (OP == CMP_F32_SGPR) asm volatile("v_cmp_lt_f32_e64 %0, %1, %2" : "=s"(m[i & 3]) : "v"(f[i]), "v"(fy));
     if constexpr (OP == RCP_F64) asm volatile("v_rcp_f64 %0, %0" : "+v"(d[i]));
     if constexpr (OP == FRACT_F64) asm volatile("v_fract_f64 %0, %0" : "+v"(d[i]));
+    if constexpr (OP == CNDMASK_VCC) asm volatile("s_mov_b64 vcc, %1\n\tv_cndmask_b32 %0, %0, %2, vcc" : "+v"(u[i]) : "s"(mask), "v"(uy) : "vcc");
+    if constexpr (OP == CMP_U32_VCC) asm volatile("v_cmp_lt_u32 vcc, %0, %1" : : "v"(u[i]), "v"(uy) : "vcc");
+    if constexpr (OP == CMP_CLASS_F64) asm volatile("v_cmp_class_f64 vcc, %0, %1" : : "v"(d[i]), "v"(uy) : "vcc");
+    if constexpr (OP == OR_B32) asm volatile("v_or_b32 %0, %0, %1" : "+v"(u[i]) : "v"(uy));
+    if constexpr (OP == LSHR_B32_VOP2) asm volatile("v_lshrrev_b32 %0, %1, %0" : "+v"(u[i]) : "v"(uy));
+    if constexpr (OP == BFE_U32) asm volatile("v_bfe_u32 %0, %0, 3, 7" : "+v"(u[i]));
+    if constexpr (OP == MUL_LO_U32) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(u[i]) : "v"(uy));
+    if constexpr (OP == CVT_F64_I32) asm volatile("v_cvt_f64_i32 %0, %1" : "=v"(d[i]) : "v"(u[i]));
+    if constexpr (OP == LDEXP_F64) asm volatile("v_ldexp_f64 %0, %0, %1" : "+v"(d[i]) : "v"(uy));
+    if constexpr (OP == WRITELANE) asm volatile("v_writelane_b32 %0, %1, 5" : "+v"(u[i]) : "s"((uint32_t)mask));
+    if constexpr (OP == SUB_U32) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(u[i]) : "v"(uy));
+    if constexpr (OP == MAX_I32) asm volatile("v_max_i32 %0, %0, %1" : "+v"(u[i]) : "v"(uy));
   }
 }
 

@@ -144,6 +144,13 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "lb0": ["RT_NF_LB=0"],                    # nearest-first: grown-box entry by its own slab computation
     "lb1": ["RT_NF_LB=1"],                    # ... as a lower bound from the exact box's slab values
     "kd0": ["RT_KNN_DIV=0"],                  # kNN scans as packets only
+    "uo0": ["RT_UNI_OPAQUE=0"],               # uniform values hoisted (and spilled) out of the sample loop (round 5)
+    "uo1": [],                                # ... made opaque where used (uni_here, default)
+    "f320": ["RT_F32_BOX=0"],                 # box tests in fp64 only (round 5)
+    "f32nf": ["RT_F32_SHADOW=0"],             # fp32 box pre-test in the nearest-first closest hit only
+    "f32all": ["RT_F32_SHADOW_OPAQUE=1"],     # ... and in every variant's shadow traversal
+    "f32def": [],                             # ... in the transparent variants' shadow traversal (default)
+    "f32nt": ["RT_F32_SHADOW_TRANS=0"],       # ... but not in the transparent variants' shadow traversal
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
