@@ -324,13 +324,31 @@ def main():
     # the ranks' communicator (N > 1, native): RCCL over xGMI, or the host transport on gloo (rehearsals)
     native = args.impl == "native"
     comm = None
+    comm_note = None
     if world > 1 and native:
         if args.backend == "nccl":
+            # RCCL communicator of the library (its own, beside torch's); if any rank fails to make it,
+            # every rank falls back to the host transport over a gloo group (slower exchange through host
+            # memory, same frame) -- decided collectively, so no rank is left waiting
+            gloo_pg = dist.new_group(backend="gloo")
             uid = torch.zeros(128, dtype=torch.uint8, device=coll_dev)
             if rank == 0:
                 uid.copy_(torch.frombuffer(bytearray(rt.group_unique_id()), dtype=torch.uint8))
             dist.broadcast(uid, 0)
-            comm = rt.Comm.rccl(rank, world, bytes(uid.cpu().numpy().tobytes()), dev)
+            err = None
+            try:
+                comm = rt.Comm.rccl(rank, world, bytes(uid.cpu().numpy().tobytes()), dev)
+                comm.selftest(1031)
+            except rt.RTError as e:
+                err = str(e)
+            bad = torch.tensor([1 if err else 0], dtype=torch.int32)
+            dist.all_reduce(bad, group=gloo_pg)
+            if int(bad.item()):
+                if comm is not None:
+                    comm.close()
+                comm = rt.Comm.host(dist, gloo_pg)
+                comm_note = f"RCCL communicator failed on {int(bad.item())} rank(s) ({err or 'another rank'}): host transport over gloo"
+                print(f"bench.py rank {rank}: {comm_note}", file=sys.stderr)
         else:
             comm = rt.Comm.host(dist)
     photon_s = None
@@ -363,8 +381,8 @@ def main():
         my_tiles = np.concatenate([run_t, split_t]).astype(np.int32)
         parallelism = ("1 GPU" if world == 1 else
                        f"cost-balanced wave tiles over {world} ranks (native rt_group, one process per GPU) + "
-                       + ("RCCL send/recv of the ARGB pixels to rank 0" if args.backend == "nccl" else
-                          "host-transport (gloo) send/recv of the ARGB pixels to rank 0"))
+                       + ("RCCL send/recv of the ARGB pixels to rank 0" if comm is not None and comm.info()["transport"] == "rccl"
+                          else "host-transport (gloo) send/recv of the ARGB pixels to rank 0"))
 
         def step(ev=None):
             grp.render()
@@ -541,6 +559,7 @@ def main():
             "kernel_ms_max_over_ranks": kern_ms_max,
             "rank_render_ms_after_rebalance": rank_ms_rebalanced if native else None,
             "frame_check": frame_check,
+            "transport_note": comm_note,
             "host_path_ms_per_step": host_ms,
             "host_path": "rt_render into a host ARGB buffer (the JNI draw(), INTEGRATION.md): kernel + "
                          f"{W * H * 4} B read-back to pageable memory, blocking; 1-GPU runs only",
