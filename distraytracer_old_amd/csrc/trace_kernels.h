@@ -668,18 +668,20 @@ DEVI bool nf_child(const ChildBox& c, double s, double ymax, V o, V d, const Ray
 #ifndef RT_F32_BOX
 #define RT_F32_BOX 1
 #endif
-// In the shadow (any-hit) packet traversal it pays in the transparent variants (C4 484 -> 455 ms, C5
-// 175.1 -> 173.4 ms) but not in C3's triangles-only variant, whose shading code then spills (2.90 ->
-// 2.96 ms); the nearest-first closest hit gains in C3 (2.94 -> 2.90 ms). Same images
-// (profiles/r06f_f32_ab.log).
+// In the shadow (any-hit) packet traversal: C4 482 -> 453 ms, C5 175.1 -> 173.4 ms; in C3's
+// triangles-only variant only with the fp32 ray rebuilt per node from the fp64 one (RT_F32_SH_LAZY:
+// held through the traversal its registers made the shading code spill, 2.90 -> 2.96 ms; rebuilt,
+// 2.90 -> 2.87 ms, and C4 453 -> 450 ms; the photon variant keeps it held, C5 173.3 vs 174.6 ms).
+// The nearest-first closest hit gains in C3 (2.94 -> 2.90 ms). Same images (profiles/r06f_f32_ab.log,
+// r06h_f32_ab_same_box.log, r06j_f32_lazy_ab.log).
 #ifndef RT_F32_SHADOW  // the fp32 pre-test in the shadow (any-hit) packet traversal
 #define RT_F32_SHADOW 1
 #endif
 #ifndef RT_F32_SHADOW_TRANS  // ... of the transparent variants
 #define RT_F32_SHADOW_TRANS 1
 #endif
-#ifndef RT_F32_SHADOW_OPAQUE  // ... of the other variants
-#define RT_F32_SHADOW_OPAQUE 0
+#ifndef RT_F32_SHADOW_OPAQUE  // ... of the other variants (with the fp32 ray rebuilt per node, RT_F32_SH_LAZY)
+#define RT_F32_SHADOW_OPAQUE 1
 #endif
 struct RayF {
   float y[3], noy[3];  // RN(y_i), RN(-RN(o_i) RN(y_i))
@@ -694,6 +696,22 @@ DEVI RayF ray_f32(V o, const RayInv& ri, double ymax) {
   r.omax = (float)(fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z)) * (1 + 0x1p-20));
   return r;
 }
+// the per-axis part of ray_f32 alone (RT_F32_SH_LAZY)
+DEVI double opaque_d(double x) {  // kept from being hoisted out of the traversal loop
+  asm volatile("" : "+v"(x));
+  return x;
+}
+DEVI RayF ray_f32_dirs(V o, const RayInv& ri) {
+  RayF r;
+  const float ox = (float)opaque_d(o.x), oy = (float)opaque_d(o.y), oz = (float)opaque_d(o.z);
+  r.y[0] = (float)opaque_d(ri.y[0]); r.y[1] = (float)opaque_d(ri.y[1]); r.y[2] = (float)opaque_d(ri.y[2]);
+  r.noy[0] = -(ox * r.y[0]); r.noy[1] = -(oy * r.y[1]); r.noy[2] = -(oz * r.y[2]);
+  r.ymax = r.omax = 0;
+  return r;
+}
+#ifndef RT_F32_SH_LAZY  // (variants without a photon map)
+#define RT_F32_SH_LAZY 1
+#endif
 DEVI float f32_margin(const RayF& r, float mag) { return 0x1p-20f * (r.ymax * (mag + r.omax)); }
 enum : int { B32_MISS = 0, B32_HIT = 1, B32_OPEN = 2 };
 // b: min[3] max[3] of one child (fp32); lo: the fp32 entry (a settled hit's entry within E)
@@ -1231,6 +1249,9 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
   // settled when the entry is certain to lie clear of dist - EPS (bracketed here by 2^-20 of it)
   constexpr bool F32 = RT_F32_BOX && RT_F32_SHADOW && ((F & FT_TRANS) != 0 ? RT_F32_SHADOW_TRANS : RT_F32_SHADOW_OPAQUE);
   const bool f32 = F32 && ri.fast;
+  // RT_F32_SH_LAZY: only the margin's two ray terms and the distance bracket live across the
+  // traversal; the fp32 ray itself is rebuilt from the fp64 one (live anyway) at each node -- fewer
+  // registers held through the shading code the traversal is inlined into
   RayF rf;
   float dLo = 0, dHi = 0;
   if constexpr (F32) {
@@ -1269,6 +1290,11 @@ DEVI bool accel_any_pk(const SceneD& S, const AccelD& A, V ao, V ad, WRay& w, co
         if (in_mask_t<MASKOPS<F>>(act)) {
           if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX]++; }
           if (f32) {
+            if constexpr (RT_F32_SH_LAZY != 0 && (F & FT_PHOTON) == 0) {
+              const RayF r2 = ray_f32_dirs(ao, ri);
+              rf.y[0] = r2.y[0]; rf.y[1] = r2.y[1]; rf.y[2] = r2.y[2];
+              rf.noy[0] = r2.noy[0]; rf.noy[1] = r2.noy[1]; rf.noy[2] = r2.noy[2];
+            }
             const float E = f32_margin(rf, nb.mag);
             float lo;
             const int c0 = box32(nb.b, rf, E, lo);

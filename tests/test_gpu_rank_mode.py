@@ -66,6 +66,14 @@ def test_rank_mode_host_transport_reassembles_the_frame(tmp_path, case, world):
         assert "photon_list and map == rt_photons_build" in names
 
 
+def test_rank_mode_host_transport_c4_scene(tmp_path):
+    """C4's variant (glass, image / marble textures, spot lights) in rank mode: 2 ranks."""
+    rep = _run(2, ["--cli", "plnts3ColsBunnies.cli", "--width", "256", "--height", "256", "--spp", "2",
+                   "--seed", str(0x5EED0004), "--transport", "host"], tmp_path)
+    _assert_checks(rep)
+    assert "every frame == rt_render bit for bit" in [c[0] for c in rep["checks"]]
+
+
 def test_rank_mode_mismatched_frame_fails_on_every_rank(tmp_path):
     rep = _run(2, CASES["c3"] + ["--transport", "host", "--mismatch"], tmp_path)
     _assert_checks(rep)

@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 6: full GPU suite + smoke + C3/C4/C5 bench lines + C3 profile of build c31eeff2 (lazy shadow pre-test)
+set -o pipefail
+OUT=gpurun_out/r06l
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 1000 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $OUT/pytest_gpu.log 2>&1 && \
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
+bash tools/gpu_prof_cfg.sh C3 r06l/c3 20 && \
+timeout -k 10 300 python3 bench.py > $OUT/bench_c3.json 2> $OUT/bench_c3.err && \
+timeout -k 10 300 python3 bench.py --config C5 --no-cpu-baseline --steps 5 > $OUT/bench_c5.json 2> $OUT/bench_c5.err && \
+timeout -k 10 400 python3 bench.py --config C4 --no-cpu-baseline --steps 3 > $OUT/bench_c4.json 2> $OUT/bench_c4.err
+echo "exit $?" >> $OUT/status.txt

@@ -151,6 +151,9 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "f32all": ["RT_F32_SHADOW_OPAQUE=1"],     # ... and in every variant's shadow traversal
     "f32def": [],                             # ... in the transparent variants' shadow traversal (default)
     "f32nt": ["RT_F32_SHADOW_TRANS=0"],       # ... but not in the transparent variants' shadow traversal
+    "lz0": ["RT_F32_SH_LAZY=0"],              # shadow fp32 pre-test with the fp32 ray held through the traversal
+    "lz": [],                                 # ... rebuilt per node from the fp64 ray (default)
+    "lzop": ["RT_F32_SHADOW_OPAQUE=1"],       # ... and in the opaque variants' (C3's) shadow traversal too
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
