@@ -509,6 +509,104 @@ struct PkStack {
   DEVI int32_t getC(int i) const { return uni(pkC()[i]); }
 };
 
+// ---- conservative fp32 box pre-test (RT_F32_BOX) ---------------------------------------------
+// The packet traversals' child-box tests first run in fp32 on the node's fp32 boxes (NodeF): a
+// wave64 f32 fma / add / min is issued at twice the rate of its fp64 form on gfx950, and the whole
+// test is ~22 instructions instead of ~30 fp64 ones (tools/valu_issue.hip, DESIGN.md §6). A decision
+// is taken from fp32 only when it is certain, and then it is the reference's (myBBox.intersectCheck,
+// myGeomBase.java:132-162); every other lane runs the existing fp64 tests. The bound: with
+// t = (b - o) y (real, y the fp64 reciprocal), the fp32 slab value t' = fma(RN(b), RN(y), RN(-RN(o) RN(y)))
+// satisfies |t' - t| <= 2^-21 |y| (|b| + |o|) (four roundings of 2^-24, |t| <= |y| (|b| + |o|)), so with
+// E = 2^-20 ymax (mag + omax) (mag >= |b| over the node's two boxes, both bounds rounded up) the fp32
+// entry / exit lo', hi' are within E of the real ones, and each fp32 compare below rounds by at most
+// 2^-24 of values <= 2^20 E: a miss is certain when hi' < lo' - 4E or lo' < -2E, a hit when
+// hi' > lo' + 4E and lo' > 2E (the reference's own rounding, ~2^-51 relative, is far inside these
+// margins). Overflow makes E (and the test) +inf or NaN: nothing is settled then.
+#ifndef RT_F32_BOX
+#define RT_F32_BOX 1
+#endif
+// In the shadow (any-hit) packet traversal: C4 482 -> 453 ms, C5 175.1 -> 173.4 ms; in C3's
+// triangles-only variant only with the fp32 ray rebuilt per node from the fp64 one (RT_F32_SH_LAZY:
+// held through the traversal its registers made the shading code spill, 2.90 -> 2.96 ms; rebuilt,
+// 2.90 -> 2.87 ms, and C4 453 -> 450 ms; the photon variant keeps it held, C5 173.3 vs 174.6 ms).
+// The nearest-first closest hit gains in C3 (2.94 -> 2.90 ms). Same images (profiles/r06f_f32_ab.log,
+// r06h_f32_ab_same_box.log, r06j_f32_lazy_ab.log).
+#ifndef RT_F32_SHADOW  // the fp32 pre-test in the shadow (any-hit) packet traversal
+#define RT_F32_SHADOW 1
+#endif
+#ifndef RT_F32_SHADOW_TRANS  // ... of the transparent variants
+#define RT_F32_SHADOW_TRANS 1
+#endif
+#ifndef RT_F32_SHADOW_OPAQUE  // ... of the other variants (with the fp32 ray rebuilt per node, RT_F32_SH_LAZY)
+#define RT_F32_SHADOW_OPAQUE 1
+#endif
+struct RayF {
+  float y[3], noy[3];  // RN(y_i), RN(-RN(o_i) RN(y_i))
+  float ymax, omax;    // >= max |y_i|, >= max |o_i|
+};
+DEVI RayF ray_f32(V o, const RayInv& ri, double ymax) {
+  RayF r;
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  r.y[0] = (float)ri.y[0]; r.y[1] = (float)ri.y[1]; r.y[2] = (float)ri.y[2];
+  r.noy[0] = -(ox * r.y[0]); r.noy[1] = -(oy * r.y[1]); r.noy[2] = -(oz * r.y[2]);
+  r.ymax = (float)(ymax * (1 + 0x1p-20));
+  r.omax = (float)(fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z)) * (1 + 0x1p-20));
+  return r;
+}
+// the per-axis part of ray_f32 alone (RT_F32_SH_LAZY)
+DEVI double opaque_d(double x) {  // kept from being hoisted out of the traversal loop
+  asm volatile("" : "+v"(x));
+  return x;
+}
+DEVI RayF ray_f32_dirs(V o, const RayInv& ri) {
+  RayF r;
+  const float ox = (float)opaque_d(o.x), oy = (float)opaque_d(o.y), oz = (float)opaque_d(o.z);
+  r.y[0] = (float)opaque_d(ri.y[0]); r.y[1] = (float)opaque_d(ri.y[1]); r.y[2] = (float)opaque_d(ri.y[2]);
+  r.noy[0] = -(ox * r.y[0]); r.noy[1] = -(oy * r.y[1]); r.noy[2] = -(oz * r.y[2]);
+  r.ymax = r.omax = 0;
+  return r;
+}
+// The same pre-test in the reference-order closest hit of the transparent variants (RT_F32_CPK) does
+// not pay: C4 450.8 -> 451.9 ms, C5 173.1 -> 175.8 ms (profiles/r06n_f32_cpk_ab.log) -- those
+// traversals test one box per step and the fp64 box's SGPRs were already loaded; off.
+#ifndef RT_F32_CPK  // the fp32 pre-test in the reference-order closest hit of the transparent variants
+#define RT_F32_CPK 0
+#endif
+#ifndef RT_F32_CPK_PHOTON  // ... of the photon-map variant too
+#define RT_F32_CPK_PHOTON 1
+#endif
+#ifndef RT_F32_SH_LAZY  // (variants without a photon map)
+#define RT_F32_SH_LAZY 1
+#endif
+DEVI float f32_margin(const RayF& r, float mag) { return 0x1p-20f * (r.ymax * (mag + r.omax)); }
+enum : int { B32_MISS = 0, B32_HIT = 1, B32_OPEN = 2 };
+// b: min[3] max[3] of one child (fp32); lo: the fp32 entry (a settled hit's entry within E)
+DEVI int box32(const float* b, const RayF& r, float E, float& lo) {
+  const float t0 = __builtin_fmaf(b[0], r.y[0], r.noy[0]), t3 = __builtin_fmaf(b[3], r.y[0], r.noy[0]);
+  const float t1 = __builtin_fmaf(b[1], r.y[1], r.noy[1]), t4 = __builtin_fmaf(b[4], r.y[1], r.noy[1]);
+  const float t2 = __builtin_fmaf(b[2], r.y[2], r.noy[2]), t5 = __builtin_fmaf(b[5], r.y[2], r.noy[2]);
+  lo = fmaxf(fmaxf(fminf(t0, t3), fminf(t1, t4)), fminf(t2, t5));
+  const float hi = fminf(fminf(fmaxf(t0, t3), fmaxf(t1, t4)), fmaxf(t2, t5));
+  if (hi < lo - 4 * E || lo < -2 * E) return B32_MISS;
+  if (hi > lo + 4 * E && lo > 2 * E) return B32_HIT;
+  return B32_OPEN;
+}
+// nf_child's lower bound of a settled hit's grown entry: lo_real - s ymax >= (lo' - E) - s ymax, and
+// the two fp32 roundings here are covered by the further 2E and by s, ymax being rounded up
+DEVI double lb32(float lo, float E, float s, const RayF& r) { return (double)((lo - 3 * E) - s * r.ymax); }
+struct NodeBoxF {  // a node's fp32 record, scalar-loaded
+  float b[12];
+  float mag, sl, sr;
+};
+DEVI NodeBoxF sload_nodef(const NodeF* p) {
+  NodeBoxF n;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) n.b[i] = sload(p->b + i);
+  n.mag = sload(&p->mag); n.sl = sload(&p->sl); n.sr = sload(&p->sr);
+  return n;
+}
+DEVI int32_t sload_ref(const NodeD* nd, int side) { return sload(side ? &nd->right : &nd->left); }
+
 // accel_closest<INST = false> as a packet traversal (same per-lane semantics)
 template <bool CNT, uint32_t F>
 DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv ri, WRay& w, const Key& k,
@@ -519,23 +617,67 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
   uint64_t act = __ballot(1);  // lanes in the current subtree
   int32_t N = uni(A.root);
   const int32_t axf = A.xf;
+  // the fp32 box pre-test (box32) in the transparent variants, whose closest hit takes this
+  // reference-order traversal (not C3's, where it is only the fat-edge fallback)
+  constexpr bool F32 = RT_F32_BOX && RT_F32_CPK && (F & FT_TRANS) != 0 && (RT_F32_CPK_PHOTON || (F & FT_PHOTON) == 0);
+  constexpr bool LAZY = RT_F32_SH_LAZY != 0 && (F & FT_PHOTON) == 0;
+  const bool f32 = F32 && ri.fast;
+  RayF rf;
+  if constexpr (F32) rf = ray_f32(ao, ri, fmax(fmax(fabs(ri.y[0]), fabs(ri.y[1])), fabs(ri.y[2])));
+  auto rebuild = [&]() {
+    if constexpr (F32 && LAZY) {
+      const RayF r2 = ray_f32_dirs(ao, ri);
+      rf.y[0] = r2.y[0]; rf.y[1] = r2.y[1]; rf.y[2] = r2.y[2];
+      rf.noy[0] = r2.noy[0]; rf.noy[1] = r2.noy[1]; rf.noy[2] = r2.noy[2];
+    }
+  };
   while (true) {
     // descend: push N, go left with the lanes whose left box is hit
     while (N >= 0) {
-      const ChildBox cl = sload_child(S.node + N, 0);
       st.setFrame(sp, N << 1, act);
       PKSTAT(P_CB_STEP, act);
       WCNT(C_WNODE, 1);  // the node's record: left half now, right half at the unwind
       bool hl = false;
-      if (in_mask_t<MASKOPS<F>>(act)) {
-        if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }
-        st.setT(sp, local);
-        local = DMAX;
-        hl = box_hit<MASKOPS<F>>(cl.mn, cl.mx, ao, ad, ri);
+      int32_t lref;
+      if constexpr (F32) {
+        const NodeD* nd = S.node + N;
+        lref = sload_ref(nd, 0);
+        bool open = false;
+        if (in_mask_t<MASKOPS<F>>(act)) {
+          if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }
+          st.setT(sp, local);
+          local = DMAX;
+          if (f32) {
+            rebuild();
+            float b[6], mag;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) b[i] = sload(S.nodeF[N].b + i);
+            mag = sload(&S.nodeF[N].mag);
+            float lo;
+            const int c = box32(b, rf, f32_margin(rf, mag), lo);
+            hl = c == B32_HIT;
+            open = c == B32_OPEN;
+          } else {
+            open = true;
+          }
+        }
+        if (__ballot(open)) {
+          const ChildBox cl = sload_child(nd, 0);
+          if (open) hl = box_hit<MASKOPS<F>>(cl.mn, cl.mx, ao, ad, ri);
+        }
+      } else {
+        const ChildBox cl = sload_child(S.node + N, 0);
+        lref = cl.ref;
+        if (in_mask_t<MASKOPS<F>>(act)) {
+          if (CNT) { ct.c[C_NODE]++; ct.c[C_BOX] += 2; }
+          st.setT(sp, local);
+          local = DMAX;
+          hl = box_hit<MASKOPS<F>>(cl.mn, cl.mx, ao, ad, ri);
+        }
       }
       sp++;
       const uint64_t H = __ballot(hl);
-      if (H) { act = H; N = cl.ref; }
+      if (H) { act = H; N = lref; }
       else { N = INT32_MAX; break; }
     }
     if (N != INT32_MAX && in_mask_t<MASKOPS<F>>(act)) leaf_closest<CNT, F, false, true>(S, ~N, axf, ao, ad, w, k, hc, best, local, ct);
@@ -545,15 +687,49 @@ DEVI void accel_closest_pk(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
       const int32_t np = st.getN(sp - 1);
       const uint64_t M = st.getM(sp - 1);
       if ((np & 1) == 0) {
-        const ChildBox cr = sload_child(S.node + (np >> 1), 1);
         PKSTAT(P_CB_STEP, M);
         bool gr = false;
-        if (in_mask_t<MASKOPS<F>>(M)) gr = box_before<MASKOPS<F>>(cr.mn, cr.mx, ao, ad, ri, local);
+        int32_t rref;
+        if constexpr (F32) {
+          // hit and (local == DMAX or entry < local): settled when the entry is clear of local
+          const NodeD* nd = S.node + (np >> 1);
+          rref = sload_ref(nd, 1);
+          bool open = false;
+          if (in_mask_t<MASKOPS<F>>(M)) {
+            if (f32) {
+              rebuild();
+              float b[6], mag;
+#pragma unroll
+              for (int i = 0; i < 6; ++i) b[i] = sload(S.nodeF[np >> 1].b + 6 + i);
+              mag = sload(&S.nodeF[np >> 1].mag);
+              float lo;
+              const float E = f32_margin(rf, mag);
+              const int c = box32(b, rf, E, lo);
+              if (c == B32_HIT) {
+                const double lt = fabs(local) * 0x1p-40;
+                if (local == DMAX || (double)(lo + 2 * E) < local - lt) gr = true;
+                else if (!((double)(lo - 2 * E) > local + lt)) open = true;
+              } else {
+                open = c == B32_OPEN;
+              }
+            } else {
+              open = true;
+            }
+          }
+          if (__ballot(open)) {
+            const ChildBox cr = sload_child(nd, 1);
+            if (open) gr = box_before<MASKOPS<F>>(cr.mn, cr.mx, ao, ad, ri, local);
+          }
+        } else {
+          const ChildBox cr = sload_child(S.node + (np >> 1), 1);
+          rref = cr.ref;
+          if (in_mask_t<MASKOPS<F>>(M)) gr = box_before<MASKOPS<F>>(cr.mn, cr.mx, ao, ad, ri, local);
+        }
         const uint64_t R = __ballot(gr);
         if (R) {
           st.setN(sp - 1, np | 1);
           act = R;
-          N = cr.ref;
+          N = rref;
           break;
         }
       }
@@ -652,95 +828,6 @@ DEVI bool nf_child(const ChildBox& c, double s, double ymax, V o, V d, const Ray
   e = entry_grown(c.mn, c.mx, s, o, ri.y);
   return e <= lim;
 }
-// ---- conservative fp32 box pre-test (RT_F32_BOX) ---------------------------------------------
-// The packet traversals' child-box tests first run in fp32 on the node's fp32 boxes (NodeF): a
-// wave64 f32 fma / add / min is issued at twice the rate of its fp64 form on gfx950, and the whole
-// test is ~22 instructions instead of ~30 fp64 ones (tools/valu_issue.hip, DESIGN.md §6). A decision
-// is taken from fp32 only when it is certain, and then it is the reference's (myBBox.intersectCheck,
-// myGeomBase.java:132-162); every other lane runs the existing fp64 tests. The bound: with
-// t = (b - o) y (real, y the fp64 reciprocal), the fp32 slab value t' = fma(RN(b), RN(y), RN(-RN(o) RN(y)))
-// satisfies |t' - t| <= 2^-21 |y| (|b| + |o|) (four roundings of 2^-24, |t| <= |y| (|b| + |o|)), so with
-// E = 2^-20 ymax (mag + omax) (mag >= |b| over the node's two boxes, both bounds rounded up) the fp32
-// entry / exit lo', hi' are within E of the real ones, and each fp32 compare below rounds by at most
-// 2^-24 of values <= 2^20 E: a miss is certain when hi' < lo' - 4E or lo' < -2E, a hit when
-// hi' > lo' + 4E and lo' > 2E (the reference's own rounding, ~2^-51 relative, is far inside these
-// margins). Overflow makes E (and the test) +inf or NaN: nothing is settled then.
-#ifndef RT_F32_BOX
-#define RT_F32_BOX 1
-#endif
-// In the shadow (any-hit) packet traversal: C4 482 -> 453 ms, C5 175.1 -> 173.4 ms; in C3's
-// triangles-only variant only with the fp32 ray rebuilt per node from the fp64 one (RT_F32_SH_LAZY:
-// held through the traversal its registers made the shading code spill, 2.90 -> 2.96 ms; rebuilt,
-// 2.90 -> 2.87 ms, and C4 453 -> 450 ms; the photon variant keeps it held, C5 173.3 vs 174.6 ms).
-// The nearest-first closest hit gains in C3 (2.94 -> 2.90 ms). Same images (profiles/r06f_f32_ab.log,
-// r06h_f32_ab_same_box.log, r06j_f32_lazy_ab.log).
-#ifndef RT_F32_SHADOW  // the fp32 pre-test in the shadow (any-hit) packet traversal
-#define RT_F32_SHADOW 1
-#endif
-#ifndef RT_F32_SHADOW_TRANS  // ... of the transparent variants
-#define RT_F32_SHADOW_TRANS 1
-#endif
-#ifndef RT_F32_SHADOW_OPAQUE  // ... of the other variants (with the fp32 ray rebuilt per node, RT_F32_SH_LAZY)
-#define RT_F32_SHADOW_OPAQUE 1
-#endif
-struct RayF {
-  float y[3], noy[3];  // RN(y_i), RN(-RN(o_i) RN(y_i))
-  float ymax, omax;    // >= max |y_i|, >= max |o_i|
-};
-DEVI RayF ray_f32(V o, const RayInv& ri, double ymax) {
-  RayF r;
-  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
-  r.y[0] = (float)ri.y[0]; r.y[1] = (float)ri.y[1]; r.y[2] = (float)ri.y[2];
-  r.noy[0] = -(ox * r.y[0]); r.noy[1] = -(oy * r.y[1]); r.noy[2] = -(oz * r.y[2]);
-  r.ymax = (float)(ymax * (1 + 0x1p-20));
-  r.omax = (float)(fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z)) * (1 + 0x1p-20));
-  return r;
-}
-// the per-axis part of ray_f32 alone (RT_F32_SH_LAZY)
-DEVI double opaque_d(double x) {  // kept from being hoisted out of the traversal loop
-  asm volatile("" : "+v"(x));
-  return x;
-}
-DEVI RayF ray_f32_dirs(V o, const RayInv& ri) {
-  RayF r;
-  const float ox = (float)opaque_d(o.x), oy = (float)opaque_d(o.y), oz = (float)opaque_d(o.z);
-  r.y[0] = (float)opaque_d(ri.y[0]); r.y[1] = (float)opaque_d(ri.y[1]); r.y[2] = (float)opaque_d(ri.y[2]);
-  r.noy[0] = -(ox * r.y[0]); r.noy[1] = -(oy * r.y[1]); r.noy[2] = -(oz * r.y[2]);
-  r.ymax = r.omax = 0;
-  return r;
-}
-#ifndef RT_F32_SH_LAZY  // (variants without a photon map)
-#define RT_F32_SH_LAZY 1
-#endif
-DEVI float f32_margin(const RayF& r, float mag) { return 0x1p-20f * (r.ymax * (mag + r.omax)); }
-enum : int { B32_MISS = 0, B32_HIT = 1, B32_OPEN = 2 };
-// b: min[3] max[3] of one child (fp32); lo: the fp32 entry (a settled hit's entry within E)
-DEVI int box32(const float* b, const RayF& r, float E, float& lo) {
-  const float t0 = __builtin_fmaf(b[0], r.y[0], r.noy[0]), t3 = __builtin_fmaf(b[3], r.y[0], r.noy[0]);
-  const float t1 = __builtin_fmaf(b[1], r.y[1], r.noy[1]), t4 = __builtin_fmaf(b[4], r.y[1], r.noy[1]);
-  const float t2 = __builtin_fmaf(b[2], r.y[2], r.noy[2]), t5 = __builtin_fmaf(b[5], r.y[2], r.noy[2]);
-  lo = fmaxf(fmaxf(fminf(t0, t3), fminf(t1, t4)), fminf(t2, t5));
-  const float hi = fminf(fminf(fmaxf(t0, t3), fmaxf(t1, t4)), fmaxf(t2, t5));
-  if (hi < lo - 4 * E || lo < -2 * E) return B32_MISS;
-  if (hi > lo + 4 * E && lo > 2 * E) return B32_HIT;
-  return B32_OPEN;
-}
-// nf_child's lower bound of a settled hit's grown entry: lo_real - s ymax >= (lo' - E) - s ymax, and
-// the two fp32 roundings here are covered by the further 2E and by s, ymax being rounded up
-DEVI double lb32(float lo, float E, float s, const RayF& r) { return (double)((lo - 3 * E) - s * r.ymax); }
-struct NodeBoxF {  // a node's fp32 record, scalar-loaded
-  float b[12];
-  float mag, sl, sr;
-};
-DEVI NodeBoxF sload_nodef(const NodeF* p) {
-  NodeBoxF n;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) n.b[i] = sload(p->b + i);
-  n.mag = sload(&p->mag); n.sl = sload(&p->sl); n.sr = sload(&p->sr);
-  return n;
-}
-DEVI int32_t sload_ref(const NodeD* nd, int side) { return sload(side ? &nd->right : &nd->left); }
-
 // a candidate t worth the inside test: it can beat (or, by leaf order, tie) this accel's best
 // and beats the best of the entries before it (their ties win: TreeMap keeps the first)
 struct LimNF {

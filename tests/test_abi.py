@@ -28,8 +28,12 @@ def test_library_exports_every_declared_symbol():
     assert set(names) == set(rt.EXPORTS)
     assert L.rt_abi_version() == 7
     # provenance: the library carries the build id of the sources and flags it was built from
+    # (a DISTRAYTRACER_LIB override -- a tuning or sanitizer build -- carries its own defines' id)
+    import os
+
     from distraytracer_old_amd import build
-    assert rt.build_id() == build.built_id() == build.build_id()
+    if not os.environ.get("DISTRAYTRACER_LIB"):
+        assert rt.build_id() == build.built_id() == build.build_id()
 
 
 def test_no_gpu_fails_loudly():

@@ -154,6 +154,9 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "lz0": ["RT_F32_SH_LAZY=0"],              # shadow fp32 pre-test with the fp32 ray held through the traversal
     "lz": [],                                 # ... rebuilt per node from the fp64 ray (default)
     "lzop": ["RT_F32_SHADOW_OPAQUE=1"],       # ... and in the opaque variants' (C3's) shadow traversal too
+    "cpk0": ["RT_F32_CPK=0"],                 # reference-order closest hit (transparent variants): fp64 box tests
+    "cpk": [],                                # ... with the fp32 pre-test (default)
+    "cpkph0": ["RT_F32_CPK_PHOTON=0"],        # ... but not in the photon-map variant
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
