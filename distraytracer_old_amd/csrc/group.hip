@@ -146,11 +146,12 @@ struct GRank {
   int32_t *dTiles = nullptr, *dPix = nullptr, *dAll = nullptr;
   double* smpCol = nullptr;
   uint8_t* smpTr = nullptr;
-  float* fRgb = nullptr;  // whole-frame render target (ranks > 0)
-  int32_t* fArgb = nullptr;
+  float* fRgb[2] = {};  // whole-frame render targets of frames f and f + 1 (ranks > 0): frame f's pack (on
+  int32_t* fArgb[2] = {};  // the exchange stream) reads one while frame f + 1 renders into the other
   float* sRgb[2] = {};
   int32_t* sArgb[2] = {};
-  hipEvent_t evStart = nullptr, evSide = nullptr, evPacked = nullptr, evSent[2] = {}, evRendered = nullptr;
+  hipEvent_t evStart = nullptr, evSide = nullptr, evSent[2] = {}, evRendered = nullptr;
+  hipEvent_t evFree[2] = {};  // render target b read by its pack (the render of frame f + 2 may start)
   hipEvent_t tA[KRING] = {}, tB[KRING] = {};
   int64_t timed = 0;  // frames with kernel events since the last rt_group_kernel_ms
   ncclComm_t nccl = nullptr;  // RCCL transport: this rank's communicator (rank mode: the rt_comm's, borrowed)
@@ -249,16 +250,18 @@ int setup_streams(rt_group* g) {
     GCHK(hipStreamCreateWithFlags(&R.cs, hipStreamNonBlocking));
     GCHK(hipEventCreateWithFlags(&R.evStart, hipEventDisableTiming));
     GCHK(hipEventCreateWithFlags(&R.evSide, hipEventDisableTiming));
-    GCHK(hipEventCreateWithFlags(&R.evPacked, hipEventDisableTiming));
     GCHK(hipEventCreateWithFlags(&R.evRendered, hipEventDisableTiming));
+    for (int b = 0; b < 2; ++b) GCHK(hipEventCreateWithFlags(&R.evFree[b], hipEventDisableTiming));
     for (int b = 0; b < 2; ++b) GCHK(hipEventCreateWithFlags(&R.evSent[b], hipEventDisableTiming));
     for (int k = 0; k < KRING; ++k) {
       GCHK(hipEventCreate(&R.tA[k]));
       GCHK(hipEventCreate(&R.tB[k]));
     }
     if (R.rank != 0) {
-      if ((rc = gmalloc(g, (void**)&R.fArgb, npx * sizeof(int32_t)))) return rc;
-      if (g->rgb && (rc = gmalloc(g, (void**)&R.fRgb, npx * 3 * sizeof(float)))) return rc;
+      for (int b = 0; b < (g->world > 1 ? 2 : 1); ++b) {
+        if ((rc = gmalloc(g, (void**)&R.fArgb[b], npx * sizeof(int32_t)))) return rc;
+        if (g->rgb && (rc = gmalloc(g, (void**)&R.fRgb[b], npx * 3 * sizeof(float)))) return rc;
+      }
     }
   }
   if (g->root) {
@@ -466,16 +469,26 @@ int enqueue_render(rt_group* g, GRank& R, float* rgb, int32_t* argb, bool timed)
   return RT_OK;
 }
 
-// rank R (> 0): pack its pixels of frame buffer b's send slab (after the send that last used it)
+// rank R (> 0): frame f's render into target b on R.st, after frame f - 2's pack has read it
+int enqueue_rank_render(rt_group* g, GRank& R, int b, bool timed) {
+  GCHK(hipSetDevice(R.dev));
+  GCHK(hipStreamWaitEvent(R.st, R.evFree[b], 0));
+  return enqueue_render(g, R, R.fRgb[b], R.fArgb[b], timed);
+}
+
+// rank R (> 0): pack its pixels of render target b into send slab b on the exchange stream, once the
+// render is done -- off the render stream, so the next frame's render starts at once. The exchange
+// stream's own order puts it after the send that last used slab b.
 int enqueue_pack(rt_group* g, GRank& R, int b) {
   const int n = (int)R.hAll.size();
-  if (n == 0) return RT_OK;
-  GCHK(hipStreamWaitEvent(R.st, R.evSent[b], 0));
-  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, R.st, R.fArgb, R.fRgb, R.dAll, n,
-                     R.sArgb[b], g->rgb ? R.sRgb[b] : nullptr);
-  GCHK(hipGetLastError());
-  GCHK(hipEventRecord(R.evPacked, R.st));
-  GCHK(hipStreamWaitEvent(R.cs, R.evPacked, 0));
+  GCHK(hipEventRecord(R.evRendered, R.st));
+  GCHK(hipStreamWaitEvent(R.cs, R.evRendered, 0));
+  if (n > 0) {
+    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, R.cs, R.fArgb[b], R.fRgb[b], R.dAll, n,
+                       R.sArgb[b], g->rgb ? R.sRgb[b] : nullptr);
+    GCHK(hipGetLastError());
+  }
+  GCHK(hipEventRecord(R.evFree[b], R.cs));
   return RT_OK;
 }
 
@@ -500,9 +513,11 @@ int group_frame(rt_group* g, float* rgb, int32_t* argb) {
   int rc;
   // renders (+ packs) of every local rank
   for (GRank& R : g->r) {
-    const bool r0 = R.rank == 0;
-    if ((rc = enqueue_render(g, R, r0 ? rgb : R.fRgb, r0 ? argb : R.fArgb, true))) return rc;
-    if (!r0 && g->world > 1 && (rc = enqueue_pack(g, R, b))) return rc;
+    if (R.rank == 0) {
+      if ((rc = enqueue_render(g, R, rgb, argb, true))) return rc;
+    } else if ((rc = enqueue_rank_render(g, R, b, true)) || (rc = enqueue_pack(g, R, b))) {
+      return rc;
+    }
   }
   GRank* R0 = g->root ? local_rank(g, 0) : nullptr;
   if (g->world > 1) {
@@ -630,7 +645,7 @@ int destroy_group(rt_group* g) {
   for (GRank& R : g->r) {
     (void)hipSetDevice(R.dev);
     if (R.nccl && !g->rankMode && g_rccl.ok) (void)g_rccl.commDestroy(R.nccl);  // rank mode: the rt_comm's
-    for (hipEvent_t e : {R.evStart, R.evSide, R.evPacked, R.evRendered, R.evSent[0], R.evSent[1]})
+    for (hipEvent_t e : {R.evStart, R.evSide, R.evRendered, R.evSent[0], R.evSent[1], R.evFree[0], R.evFree[1]})
       if (e) (void)hipEventDestroy(e);
     for (int k = 0; k < KRING; ++k) {
       if (R.tA[k]) (void)hipEventDestroy(R.tA[k]);
@@ -939,7 +954,7 @@ int rt_group_time_rank(rt_group* g, int rank, int warmup, int iters, double* ste
       GCHK(hipEventRecord(g->evRecv[b], R0->cs));
       return RT_OK;
     }
-    if ((rc = enqueue_render(g, *R, R->fRgb, R->fArgb, true)) || (rc = enqueue_pack(g, *R, b))) return rc;
+    if ((rc = enqueue_rank_render(g, *R, b, true)) || (rc = enqueue_pack(g, *R, b))) return rc;
     const size_t n = R->hAll.size();
     GCHK(hipStreamWaitEvent(R->cs, g->evRecv[b], 0));
     if (n) {
@@ -1001,12 +1016,12 @@ int rt_group_rebalance(rt_group* g, int rounds, int iters, double* rank_ms) {
       for (GRank& R : g->r) {
         const bool r0 = R.rank == 0;
         for (int i = 0; i < 3; ++i)
-          if ((rc = enqueue_render(g, R, r0 ? g->outRgb : R.fRgb, r0 ? g->outArgb : R.fArgb, false))) return rc;
+          if ((rc = enqueue_render(g, R, r0 ? g->outRgb : R.fRgb[0], r0 ? g->outArgb : R.fArgb[0], false))) return rc;
         GCHK(hipSetDevice(R.dev));
         GCHK(hipStreamSynchronize(R.st));
         R.timed = 0;
         for (int i = 0; i < iters; ++i)
-          if ((rc = enqueue_render(g, R, r0 ? g->outRgb : R.fRgb, r0 ? g->outArgb : R.fArgb, true))) return rc;
+          if ((rc = enqueue_render(g, R, r0 ? g->outRgb : R.fRgb[0], r0 ? g->outArgb : R.fArgb[0], true))) return rc;
         int fr = 0;
         if ((rc = rt_group_kernel_ms(g, R.rank, &T[R.rank], &fr))) return rc;
       }
