@@ -660,7 +660,7 @@ extern "C" int rt_scene_inspect_cli(const char* scene_dir, const char* cli_file,
   HostScene hs;
   rc = build_host_scene(&L.d, hs);
   if (rc) return rc;
-  int64_t bytes = (int64_t)(hs.xf.size() * sizeof(XformD) + hs.tri.size() * sizeof(TriD) + hs.prim.size() * sizeof(PrimD) +
+  int64_t bytes = (int64_t)(hs.xf.size() * sizeof(XformD) + hs.tri.size() * (sizeof(TriD) + sizeof(TriF)) + hs.prim.size() * sizeof(PrimD) +
                             hs.node.size() * (sizeof(NodeD) + sizeof(NodeF)) + hs.leaf.size() * sizeof(LeafD) + hs.member.size() * 4 +
                             hs.accel.size() * sizeof(AccelD) + hs.top.size() * sizeof(TopD) + hs.mat.size() * sizeof(MatD) +
                             hs.light.size() * sizeof(LightD) + hs.texel.size() * 4);

@@ -74,6 +74,19 @@ struct NodeF {
   float mag, sl, sr, pad;
 };
 static_assert(sizeof(NodeF) == 64, "NodeF is one 64-B line");
+// fp32 record of a TriD for the conservative fp32 edge pre-test of the packet traversals
+// (trace_kernels.h tri_f32_out): m[j] = e_j x n with e_j = v_j - v_{j-1}, c[j] = v_j . m[j], n and dA
+// rounded to nearest; k >= 2^-17 max_j |m_j| max(1, |n|) and tm >= max(|v_j|, |dA|) rounded up --
+// k = +inf where a value is not finite or does not fit a float (the pre-test then rejects nothing)
+struct TriF {
+  float m[3][3];
+  float c[3];
+  float n[3];
+  float d;
+  float k, tm;
+  float pad[2];
+};
+static_assert(sizeof(TriF) == 80, "TriF");
 struct LeafD {
   int32_t start, count;  // range in leaf member refs (>= 0 tri index, < 0 ~prim index)
 };
@@ -159,6 +172,7 @@ static constexpr int KD_PER_NODED = (int)(sizeof(NodeD) / sizeof(KdNodeD));
 struct SceneD {
   const XformD* xf;
   const TriD* tri;
+  const TriF* triF;     // [ntri] fp32 edge records (tri_f32_out)
   const double* triUV;  // [ntri][3][2] texture_coord, nullptr when no triangle is image-textured
   const PrimD* prim;
   const NodeD* node;

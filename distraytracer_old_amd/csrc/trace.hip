@@ -273,6 +273,34 @@ static int upload_scene(rt_scene* s) {
       nf[i].pad = 0;
     }
     if ((rc = upload(s, nf, &d.nodeF))) return rc;
+    // fp32 edge records of the triangles (trace_kernels.h tri_f32_out)
+    std::vector<TriF> tf(h.tri.size());
+    for (size_t i = 0; i < h.tri.size(); ++i) {
+      const TriD& t = h.tri[i];
+      TriF& r = tf[i];
+      double mmax = 0, tm = std::fabs(t.dA);
+      bool fin = std::isfinite(t.dA);
+      for (int j = 0; j < 3; ++j) {
+        const double* a = t.v[j];
+        const double* b = t.v[(j + 2) % 3];
+        const double e[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+        const double m[3] = {e[1] * t.n[2] - e[2] * t.n[1], e[2] * t.n[0] - e[0] * t.n[2], e[0] * t.n[1] - e[1] * t.n[0]};
+        const double c = a[0] * m[0] + a[1] * m[1] + a[2] * m[2];
+        for (int q = 0; q < 3; ++q) { r.m[j][q] = f32(m[q]); fin = fin && std::isfinite(m[q]) && std::isfinite(a[q]); }
+        r.c[j] = f32(c);
+        r.n[j] = f32(t.n[j]);
+        fin = fin && std::isfinite(c) && std::isfinite(t.n[j]);
+        mmax = std::max(mmax, std::sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]));
+        tm = std::max(tm, std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]));
+      }
+      const double nmag = std::sqrt(t.n[0] * t.n[0] + t.n[1] * t.n[1] + t.n[2] * t.n[2]);
+      r.d = f32(t.dA);
+      r.k = fin && std::isfinite(mmax) && std::isfinite(nmag) ? f32_up(0x1p-17 * mmax * std::max(1.0, nmag)) : INFINITY;
+      r.tm = std::isfinite(tm) ? f32_up(tm) : INFINITY;
+      r.pad[0] = r.pad[1] = 0;
+      if (!std::isfinite(r.tm)) r.k = INFINITY;
+    }
+    if ((rc = upload(s, tf, &d.triF))) return rc;
   }
   d.triUV = nullptr;
   {  // triangle UVs only matter for image-textured triangles
@@ -1278,9 +1306,9 @@ int rt_render_pass(rt_scene* s, const rt_render_params* p, int step, int skip_or
 }
 
 #ifdef RT_PROF_PKSTAT
-int rt_prof_pkstat_get(uint64_t* out) {  // profiling builds only: read and clear rt_pk_stat[12]
-  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(dv::rt_pk_stat), 12 * sizeof(uint64_t)));
-  const uint64_t z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+int rt_prof_pkstat_get(uint64_t* out) {  // profiling builds only: read and clear rt_pk_stat[16]
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(dv::rt_pk_stat), 16 * sizeof(uint64_t)));
+  const uint64_t z[16] = {};
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dv::rt_pk_stat), z, sizeof(z)));
   return RT_OK;
 }

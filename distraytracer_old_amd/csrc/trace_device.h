@@ -133,7 +133,9 @@ DEVI void renorm(WRay& r) {
 // wave steps and the lanes testing in them: closest box / triangle, any-hit box / triangle
 // + closest-hit calls of the shading tree (one per traced camera / secondary ray) and shadow-ray calls
 enum { P_CB_STEP = C_N, P_CB_LANES, P_CT_STEP, P_CT_LANES, P_AB_STEP, P_AB_LANES, P_AT_STEP, P_AT_LANES,
-       P_RAY_STEP, P_RAY_LANES, P_SH_STEP, P_SH_LANES, P_N };
+       P_RAY_STEP, P_RAY_LANES, P_SH_STEP, P_SH_LANES,
+       P_CTH_STEP, P_CTH_LANES, P_ATH_STEP, P_ATH_LANES,  // triangle wave steps with a hitting lane
+       P_N };
 #else
 enum { P_N = C_N };
 #endif

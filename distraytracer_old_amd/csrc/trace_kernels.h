@@ -177,7 +177,7 @@ DEVI bool in_mask(uint64_t m) { return in_mask_t<>(m); }
 template <uint32_t F>
 static constexpr bool MASKOPS = RT_MASKOPS == 2 || (RT_MASKOPS == 1 && (F & FT_TRANS) == 0);
 #ifdef RT_PROF_PKSTAT
-__device__ unsigned long long rt_pk_stat[12];
+__device__ unsigned long long rt_pk_stat[16];
 // one wave step testing the lanes in m: counted once per wave (by its first active lane)
 #define PKSTAT(step, m)                                                                   \
   do {                                                                                    \
@@ -187,8 +187,15 @@ __device__ unsigned long long rt_pk_stat[12];
       ct.c[step + 1] += __builtin_popcountll(pk_m_);                                      \
     }                                                                                     \
   } while (0)
+// a wave step in which some lane's condition c holds, and those lanes
+#define PKSTAT_HIT(step, c)                                                               \
+  do {                                                                                    \
+    const uint64_t pk_h_ = __ballot(c);                                                   \
+    if (pk_h_) PKSTAT(step, pk_h_);                                                       \
+  } while (0)
 #else
 #define PKSTAT(step, m) do {} while (0)
+#define PKSTAT_HIT(step, c) do {} while (0)
 #endif
 #ifdef RT_PROF_REGIONS
 // profiling builds only (tools/regions.py): shader-clock cycles a wave spends in each region,
@@ -212,6 +219,77 @@ __device__ unsigned long long rt_prof_reg[R_N];
 #define PROF_ADD(v, r) do {} while (0)
 #define PROF_CNT(r) do {} while (0)
 #endif
+
+DEVI double opaque_d(double x) {  // kept from being hoisted out of the traversal loop
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// ---- conservative fp32 triangle pre-test (RT_F32_TRI) ------------------------------------------
+// Most wave steps of the packet traversals' triangle tests have no lane that hits (C3: 83 % of the
+// nearest-first closest-hit steps, 82 % of the shadow steps; profiles/r06v_pkstat_c3.json), yet each
+// runs the fp64 test with its IEEE division (planar_test; myPlanarObject.java:165-211). A lane is
+// first tested in fp32 against the triangle's edges, without the division, and counted out only when
+// that is certain; a wave whose lanes are all out skips the fp64 test. The reference's edge value at
+// its hit point is, in real arithmetic, g_j = (p - v_j) x e_j . n with p = o + t d, t = -(n.o + dA) / s,
+// s = n.d (the same for both vertex orders of Q5), and it rejects when g_j < -EPS. Scaled by |s|:
+//   G_j = g_j |s| = |s| (o.m_j - c_j) - sign(s) (n.o + dA) (d.m_j),  m_j = e_j x n,  c_j = v_j.m_j,
+// a polynomial in the fp32-rounded inputs. Its fp32 value is within 28 u |m_j| max(1,|n|) |d| (|o| + tm)
+// of the real one (u = 2^-24: input roundings plus the fma chain), the reference's own fp64 value of
+// g_j |s| within ~2^-50 of the same scale; TriF.k = 2^-17 |m|max max(1,|n|) covers both with a 4x
+// margin (|o|, |d| taken as 1-norms >= the 2-norms), 2^-40 |d| the fp32 rounding of EPS |s|, 2^-100
+// the flushed denormals. So G'_j < -(EPS |s'| + B) implies g_j < -EPS: the reference's test fails on
+// that edge whatever its t -- the lane's result is false, which is all the pre-test ever decides.
+// It decides nothing where s' is within its rounding of 0 (the sign of s could differ) or B is large
+// enough for a product to overflow; a non-finite record has k = +inf (B = +inf or NaN: no compare holds).
+#ifndef RT_F32_TRI
+#define RT_F32_TRI 1
+#endif
+#ifndef RT_F32_TRI_CPK  // ... in the reference-order closest hit (leaf_closest) too
+#define RT_F32_TRI_CPK 1
+#endif
+struct TriRayF {
+  float o[3], d[3];
+  float O, D;  // |o'|_1, |d'|_1
+};
+DEVI TriRayF tri_ray_f32(V o, V d) {  // opaque: built per leaf, not hoisted and held through the traversal
+  TriRayF r;
+  r.o[0] = (float)opaque_d(o.x); r.o[1] = (float)opaque_d(o.y); r.o[2] = (float)opaque_d(o.z);
+  r.d[0] = (float)opaque_d(d.x); r.d[1] = (float)opaque_d(d.y); r.d[2] = (float)opaque_d(d.z);
+  r.O = fabsf(r.o[0]) + fabsf(r.o[1]) + fabsf(r.o[2]);
+  r.D = fabsf(r.d[0]) + fabsf(r.d[1]) + fabsf(r.d[2]);
+  return r;
+}
+struct TriFR {  // a TriF, scalar-loaded
+  float m[9], c[3], n[3], d, k, tm;
+};
+DEVI TriFR sload_trif(const TriF* p) {
+  TriFR t;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) t.m[i] = sload(&p->m[0][0] + i);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { t.c[i] = sload(p->c + i); t.n[i] = sload(p->n + i); }
+  t.d = sload(&p->d); t.k = sload(&p->k); t.tm = sload(&p->tm);
+  return t;
+}
+static constexpr float EPS_F32_UP = 1.00000001168609742e-07f;  // RN(1e-7) >= EPS
+// true: the reference's triangle test certainly returns false for this lane
+DEVI bool tri_f32_out(const TriFR& T, const TriRayF& r) {
+  const float s = __builtin_fmaf(T.n[2], r.d[2], __builtin_fmaf(T.n[1], r.d[1], T.n[0] * r.d[0]));
+  const float P = __builtin_fmaf(T.n[2], r.o[2], __builtin_fmaf(T.n[1], r.o[1], __builtin_fmaf(T.n[0], r.o[0], T.d)));
+  const float as = fabsf(s), sP = s < 0 ? -P : P;
+  const float B = __builtin_fmaf(r.D, __builtin_fmaf(T.k, r.O + T.tm, 0x1p-40f), 0x1p-100f);
+  const float thr = -__builtin_fmaf(EPS_F32_UP, as, B);
+  bool out = false;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float* m = T.m + 3 * j;
+    const float Q = __builtin_fmaf(m[2], r.o[2], __builtin_fmaf(m[1], r.o[1], __builtin_fmaf(m[0], r.o[0], -T.c[j])));
+    const float R = __builtin_fmaf(m[2], r.d[2], __builtin_fmaf(m[1], r.d[1], m[0] * r.d[0]));
+    out = out || (__builtin_fmaf(as, Q, -(sP * R)) < thr);
+  }
+  return out && as > 0x1p-20f * r.D && B < 0x1p100f;
+}
 
 // a primitive test whose triangle record is loaded at a wave-uniform address (PK)
 template <bool CNT, uint32_t F, bool PK, class LIM = LimNone>
@@ -272,6 +350,10 @@ DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRa
                        Best& best, double& local, Counters& ct) {
   const LeafR lf = leaf_of<PK>(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
+  // the fp32 triangle pre-test (members in the accel's CTM; RT_F32_TRI_CPK)
+  constexpr bool TF32 = PK && !INST && RT_F32_TRI != 0 && RT_F32_TRI_CPK != 0;
+  TriRayF trf;
+  if constexpr (TF32) trf = tri_ray_f32(ao, ad);
   for (int i = 0; i < lf.count; ++i) {
     if (PK) PKSTAT(P_CT_STEP, __ballot(1));
     int32_t ref = leaf_member<PK>(S, lf, i);
@@ -292,7 +374,20 @@ DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRa
     } else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
     double t;
     int args;
-    if (test_ref_u<CNT, F, PK>(S, ref, o, d, k, t, args, ct, LimClosest{local, best.t})) {
+    bool th;
+    if (TF32 && (!(F & FT_PRIM) || ref >= 0) && xf == accXf && !w.moved) {  // test_ref_u's triangle case
+      if (CNT) ct.c[C_TRI]++;
+      WCNT(C_WTRI, 1);
+      const TriFR TF = sload_trif(S.triF + ref);
+      th = false;
+      if (!tri_f32_out(TF, trf)) {
+        const TriG T = sload_tri(S.tri + ref);
+        th = tri_test(T, o, d, t, args, LimClosest{local, best.t});
+      }
+    } else {
+      th = test_ref_u<CNT, F, PK>(S, ref, o, d, k, t, args, ct, LimClosest{local, best.t});
+    }
+    if (th) {
       if (t < local) local = t;
       if (t < best.t) {
         best.t = t; best.ref = ref; best.top = (int16_t)hc.top; best.inAcc = 1; best.inst = hc.inst;
@@ -554,10 +649,6 @@ DEVI RayF ray_f32(V o, const RayInv& ri, double ymax) {
   return r;
 }
 // the per-axis part of ray_f32 alone (RT_F32_SH_LAZY)
-DEVI double opaque_d(double x) {  // kept from being hoisted out of the traversal loop
-  asm volatile("" : "+v"(x));
-  return x;
-}
 DEVI RayF ray_f32_dirs(V o, const RayInv& ri) {
   RayF r;
   const float ox = (float)opaque_d(o.x), oy = (float)opaque_d(o.y), oz = (float)opaque_d(o.z);
@@ -606,6 +697,7 @@ DEVI NodeBoxF sload_nodef(const NodeF* p) {
   return n;
 }
 DEVI int32_t sload_ref(const NodeD* nd, int side) { return sload(side ? &nd->right : &nd->left); }
+
 
 // accel_closest<INST = false> as a packet traversal (same per-lane semantics)
 template <bool CNT, uint32_t F>
@@ -945,15 +1037,28 @@ DEVI void accel_closest_nf(const SceneD& S, const AccelD& A, V ao, V ad, RayInv 
       const int32_t c = ~N;
       const int32_t st = (c >> 5) & LEAF_RUN_MAXSTART, cnt = c & 31;
       if (CNT && in_mask_t<MASKOPS<F>>(act)) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += cnt; }
+#if RT_F32_TRI
+      const TriRayF trf = tri_ray_f32(ao, ad);
+#endif
       for (int i = 0; i < cnt; ++i) {
         PKSTAT(P_CT_STEP, act);
         WCNT(C_WTRI, 1);
+        bool need = in_mask_t<MASKOPS<F>>(act);
+        if (CNT && need) ct.c[C_TRI]++;
+#if RT_F32_TRI
+        {
+          const TriFR TF = sload_trif(S.triF + st + i);
+          if (need) need = !tri_f32_out(TF, trf);
+          if (!__ballot(need)) continue;
+        }
+#endif
         const TriG T = sload_tri(S.tri + st + i);
-        if (in_mask_t<MASKOPS<F>>(act)) {
-          if (CNT) ct.c[C_TRI]++;
+        if (need) {
           double t;
           int args;
-          if (tri_test(T, ao, ad, t, args, LimNF{bt, best.t}) && (t < bt || (t == bt && st + i < bref))) {
+          const bool th = tri_test(T, ao, ad, t, args, LimNF{bt, best.t});
+          PKSTAT_HIT(P_CTH_STEP, th);
+          if (th && (t < bt || (t == bt && st + i < bref))) {
             bt = t;
             bref = st + i;
             // the ray enters the leaf box (the reference's slab arithmetic) clearly before t
@@ -1263,6 +1368,9 @@ template <bool CNT, uint32_t F, bool INST, bool PK = false>
 DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
   const LeafR lf = leaf_of<PK>(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
+  constexpr bool TF32 = PK && RT_F32_TRI != 0;  // the fp32 triangle pre-test (members in the accel's CTM)
+  TriRayF trf;
+  if constexpr (TF32) trf = tri_ray_f32(ao, ad);
   for (int i = 0; i < lf.count; ++i) {
     if (PK) PKSTAT(P_AT_STEP, __ballot(1));
     int32_t ref = leaf_member<PK>(S, lf, i);
@@ -1283,7 +1391,21 @@ DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w
     } else { const double* inv = S.xf[xf].inv; o = xpt(inv, w.o); d = xvec(inv, w.d); }
     double t;
     int args;
-    if (test_ref_u<CNT, F, PK>(S, ref, o, d, k, t, args, ct, LimShadow{dist}) && (dist - t) > EPS) return true;
+    bool th;
+    if (TF32 && (!(F & FT_PRIM) || ref >= 0) && xf == accXf && !w.moved) {  // test_ref_u's triangle case
+      if (CNT) ct.c[C_TRI]++;
+      WCNT(C_WTRI, 1);
+      const TriFR TF = sload_trif(S.triF + ref);
+      th = false;
+      if (!tri_f32_out(TF, trf)) {
+        const TriG T = sload_tri(S.tri + ref);
+        th = tri_test(T, o, d, t, args, LimShadow{dist}) && (dist - t) > EPS;
+      }
+    } else {
+      th = test_ref_u<CNT, F, PK>(S, ref, o, d, k, t, args, ct, LimShadow{dist}) && (dist - t) > EPS;
+    }
+    if (PK) PKSTAT_HIT(P_ATH_STEP, th);
+    if (th) return true;
   }
   return false;
 }

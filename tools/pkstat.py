@@ -21,13 +21,14 @@ if len(sys.argv) > 2:
     W = H = int(sys.argv[2])
 scenes.ensure_bun69k()
 L = rt.lib()
-buf = np.zeros(12, dtype=np.uint64)
+buf = np.zeros(16, dtype=np.uint64)
 with rt.Scene.load_cli(cli, textures=scenes.prepare(cli)) as s:
     s.build_photons(seed)
     L.rt_prof_pkstat_get(ctypes.c_void_p(buf.ctypes.data))  # clear
     _, _, st = s.render_count(W, H, spp=spp, seed=seed)
     assert L.rt_prof_pkstat_get(ctypes.c_void_p(buf.ctypes.data)) == 0
-names = ["closest_box", "closest_tri", "any_box", "any_tri", "ray_calls", "shadow_calls"]
+names = ["closest_box", "closest_tri", "any_box", "any_tri", "ray_calls", "shadow_calls",
+         "closest_tri_hit", "any_tri_hit"]  # *_hit: wave steps with a hitting lane, the lanes that hit
 out = {"cfg": cfg, "W": W, "H": H, "spp": spp, "counts": st}
 for i, n in enumerate(names):
     steps, lanes = int(buf[2 * i]), int(buf[2 * i + 1])

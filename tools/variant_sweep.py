@@ -157,6 +157,8 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "cpk0": ["RT_F32_CPK=0"],                 # reference-order closest hit (transparent variants): fp64 box tests
     "cpk": [],                                # ... with the fp32 pre-test (default)
     "cpkph0": ["RT_F32_CPK_PHOTON=0"],        # ... but not in the photon-map variant
+    "tri0": ["RT_F32_TRI=0"],                 # no fp32 triangle edge pre-test
+    "tricpk0": ["RT_F32_TRI_CPK=0"],          # ... none in the reference-order closest hit
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
