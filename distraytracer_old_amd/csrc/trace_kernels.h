@@ -248,6 +248,16 @@ DEVI double opaque_d(double x) {  // kept from being hoisted out of the traversa
 #ifndef RT_F32_TRI_CPK  // ... in the reference-order closest hit (leaf_closest) too
 #define RT_F32_TRI_CPK 1
 #endif
+// Measured (same-box A/Bs, same image hashes): C3 2.867 -> 2.824 ms (nearest-first closest hit + shadow
+// rays), C4 489 -> 465 ms (+ the reference-order closest hit: 489 without it); the photon-map variant
+// loses with it in either traversal (C5 173.0 ms without, 175.6 / 175.1 ms with it in the closest hit /
+// both), so it is off there (profiles/r06w_*, r06y_f32_tri_ab.log, r06z_f32_tri_photon_ab.log)
+#ifndef RT_F32_TRI_PH_ANY  // ... in the photon-map variant's shadow rays
+#define RT_F32_TRI_PH_ANY 0
+#endif
+#ifndef RT_F32_TRI_PH_CPK  // ... in the photon-map variant's closest hit
+#define RT_F32_TRI_PH_CPK 0
+#endif
 struct TriRayF {
   float o[3], d[3];
   float O, D;  // |o'|_1, |d'|_1
@@ -351,7 +361,8 @@ DEVI void leaf_closest(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRa
   const LeafR lf = leaf_of<PK>(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
   // the fp32 triangle pre-test (members in the accel's CTM; RT_F32_TRI_CPK)
-  constexpr bool TF32 = PK && !INST && RT_F32_TRI != 0 && RT_F32_TRI_CPK != 0;
+  constexpr bool TF32 = PK && !INST && RT_F32_TRI != 0 && RT_F32_TRI_CPK != 0 &&
+                        ((F & FT_PHOTON) == 0 || RT_F32_TRI_PH_CPK != 0);
   TriRayF trf;
   if constexpr (TF32) trf = tri_ray_f32(ao, ad);
   for (int i = 0; i < lf.count; ++i) {
@@ -1368,7 +1379,8 @@ template <bool CNT, uint32_t F, bool INST, bool PK = false>
 DEVI bool leaf_any(const SceneD& S, int32_t leaf, int accXf, V ao, V ad, WRay& w, const Key& k, double dist, Counters& ct) {
   const LeafR lf = leaf_of<PK>(S, leaf);
   if (CNT) { ct.c[C_LEAF]++; ct.c[C_MEMBER] += lf.count; }
-  constexpr bool TF32 = PK && RT_F32_TRI != 0;  // the fp32 triangle pre-test (members in the accel's CTM)
+  // the fp32 triangle pre-test (members in the accel's CTM)
+  constexpr bool TF32 = PK && RT_F32_TRI != 0 && ((F & FT_PHOTON) == 0 || RT_F32_TRI_PH_ANY != 0);
   TriRayF trf;
   if constexpr (TF32) trf = tri_ray_f32(ao, ad);
   for (int i = 0; i < lf.count; ++i) {
@@ -3891,7 +3903,11 @@ render_kernel(SceneD S, ParamsD P, float* __restrict__ rgb, int32_t* __restrict_
         ks.sample = (uint32_t)s;
         if (CNT) ct.c[C_CAMERA]++;
         PROF_T0(t_smp);
+#ifdef RT_PROF_NOSAMPLE  // profiling builds only (tools/variant_sweep.py): the camera setup, sums and output alone
+        cc = mk(d.x * 1e-3, d.y * 1e-3, 0);
+#else
         cc = trace_sample<CNT, F>(S, o, d, ks, ct);
+#endif
         PROF_ADD(t_smp, R_SAMPLE);
       }
     }

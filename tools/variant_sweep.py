@@ -159,6 +159,9 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "cpkph0": ["RT_F32_CPK_PHOTON=0"],        # ... but not in the photon-map variant
     "tri0": ["RT_F32_TRI=0"],                 # no fp32 triangle edge pre-test
     "tricpk0": ["RT_F32_TRI_CPK=0"],          # ... none in the reference-order closest hit
+    "tph01": ["RT_F32_TRI_PH_ANY=0", "RT_F32_TRI_PH_CPK=1"],  # photon variant: the triangle pre-test in its closest hit
+    "tph11": ["RT_F32_TRI_PH_ANY=1", "RT_F32_TRI_PH_CPK=1"],  # ... in both traversals
+    "nosample": ["RT_PROF_NOSAMPLE"],         # camera setup, sums and output alone (results differ)
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
