@@ -162,6 +162,7 @@ VARIANTS = {  # name -> -D defines; names like "s12w4" are parsed (see defines_o
     "tph01": ["RT_F32_TRI_PH_ANY=0", "RT_F32_TRI_PH_CPK=1"],  # photon variant: the triangle pre-test in its closest hit
     "tph11": ["RT_F32_TRI_PH_ANY=1", "RT_F32_TRI_PH_CPK=1"],  # ... in both traversals
     "nosample": ["RT_PROF_NOSAMPLE"],         # camera setup, sums and output alone (results differ)
+    "pers": ["RT_PERSIST=1"],                 # persistent render launches: resident grid, tiles from a ticket counter
     "c4mr": ["@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-sched-strategy=iterative-minreg",
              "@trace.hip:-Xarch_device", "@trace.hip:-mllvm=--amdgpu-use-amdgpu-trackers=1"],
 }
@@ -216,6 +217,7 @@ def main():
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--flags", type=int, default=0)
+    ap.add_argument("--dir", default="", help="run: where the built libraries are (default tools/_variants)")
     ap.add_argument("--save", default="", help="directory: each build's frame as <name>_<cfg>.npz")
     a = ap.parse_args()
     names = a.names.split(",")
@@ -225,7 +227,7 @@ def main():
         print(json.dumps(time_one(a.cfg, a.W, a.H, a.spp, a.iters, a.flags, a.save)))
     else:
         for n in names:
-            lib = OUT / f"lib_{n}.so"
+            lib = (Path(a.dir) if a.dir else OUT) / f"lib_{n}.so"
             env = dict(os.environ, DISTRAYTRACER_LIB=str(lib))
             cmd = [sys.executable, __file__, "one", "--cfg", a.cfg, "--W", str(a.W), "--H", str(a.H), "--spp", str(a.spp),
                    "--iters", str(a.iters), "--flags", str(a.flags)]
